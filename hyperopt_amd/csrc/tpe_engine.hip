@@ -1,0 +1,830 @@
+// tpe_engine.hip -- C ABI (include/tpe_engine.h) over the gfx950 kernels.
+//
+// Host-side ownership: a tpe_engine binds one device and owns an internal
+// stream plus a cached one-hp "operator plan" used by the operator-level
+// entry points; a tpe_plan owns the device-resident history, the fitted
+// mixtures of every hp and the per-suggestion results.  No global state.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "tpe_internal.hpp"
+
+using namespace tpe;
+
+struct tpe_engine {
+  int32_t device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  tpe_plan *op = nullptr;  // cached single-hp plan for operator-level calls
+};
+
+struct tpe_plan {
+  tpe_engine *eng = nullptr;
+  int32_t P = 0;
+  int64_t ncap = 0, kcap = 0;
+  std::vector<tpe_hp> hps;
+  std::vector<int32_t> cond_parent, cond_branch;
+  std::vector<double> pprior;
+  std::vector<std::vector<int32_t>> levels;
+  std::vector<int32_t> level_off;  // offsets of each level in d_level_hps
+  struct Group { int32_t kind, off, count; };
+  std::vector<std::vector<Group>> groups;  // per level, hps grouped by lpdf kind
+  // device buffers
+  tpe_hp *d_hps = nullptr;
+  int32_t *d_cp = nullptr, *d_cb = nullptr, *d_level_hps = nullptr, *d_all_hps = nullptr;
+  double *d_pprior = nullptr;
+  double *d_losses = nullptr, *d_vals = nullptr;
+  uint8_t *d_active = nullptr, *d_below = nullptr;
+  double *d_mw = nullptr, *d_mmu = nullptr, *d_msig = nullptr, *d_scratch = nullptr;
+  MixInfo *d_info = nullptr;
+  Coef *d_coef = nullptr;
+  int64_t n = 0;  // history length
+  // suggestion state
+  int64_t s_cap = 0;
+  Partial *d_results = nullptr;
+  uint64_t *d_seeds = nullptr;
+  Partial *d_partial = nullptr;
+  size_t partial_cap = 0;
+  double *d_ext = nullptr, *d_lb = nullptr, *d_la = nullptr;
+  size_t ext_cap = 0;
+  double *d_cand = nullptr;
+  size_t cand_cap = 0;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool timed = false;
+  int64_t last_ncand = 0, last_nsug = 0;
+  int32_t last_level = -1;
+};
+
+namespace {
+
+#define CKH(expr)                                                        \
+  do {                                                                   \
+    hipError_t e_ = (expr);                                              \
+    if (e_ != hipSuccess) {                                              \
+      return fail(h, TPE_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    }                                                                    \
+  } while (0)
+
+int fail(tpe_engine *h, int code, const std::string &msg) {
+  if (h) h->err = msg;
+  return code;
+}
+
+template <typename T>
+hipError_t dalloc(T **p, size_t count) {
+  *p = nullptr;
+  if (count == 0) count = 1;
+  return hipMalloc((void **)p, count * sizeof(T));
+}
+
+void dfree(void *p) {
+  if (p) (void)hipFree(p);
+}
+
+hipStream_t pick_stream(tpe_engine *h, void *s) {
+  return s ? (hipStream_t)s : h->stream;
+}
+
+void plan_free_buffers(tpe_plan *p) {
+  void *bufs[] = {p->d_hps, p->d_cp, p->d_cb, p->d_level_hps, p->d_all_hps, p->d_pprior,
+                  p->d_losses, p->d_vals, p->d_active, p->d_below, p->d_mw, p->d_mmu,
+                  p->d_msig, p->d_scratch, p->d_info, p->d_coef, p->d_results, p->d_seeds,
+                  p->d_partial, p->d_ext, p->d_lb, p->d_la, p->d_cand};
+  for (void *b : bufs) dfree(b);
+  if (p->ev0) (void)hipEventDestroy(p->ev0);
+  if (p->ev1) (void)hipEventDestroy(p->ev1);
+}
+
+int validate_space(tpe_engine *h, const tpe_space *sp) {
+  if (!sp || sp->n_hp <= 0 || !sp->hp) return fail(h, TPE_E_INVALID, "empty space");
+  for (int i = 0; i < sp->n_hp; ++i) {
+    const tpe_hp &x = sp->hp[i];
+    if (x.family < TPE_GMM || x.family > TPE_CAT)
+      return fail(h, TPE_E_INVALID, "hp " + std::to_string(i) + ": bad family");
+    if (x.family == TPE_CAT && x.upper <= 0)
+      return fail(h, TPE_E_INVALID, "hp " + std::to_string(i) + ": categorical upper <= 0");
+    if (x.family != TPE_CAT) {
+      const bool hl = x.flags & TPE_HAS_LOW, hh = x.flags & TPE_HAS_HIGH;
+      if (hl != hh)
+        return fail(h, TPE_E_INVALID, "hp " + std::to_string(i) + ": one-sided truncation");
+      if (hl && !(x.low < x.high))
+        return fail(h, TPE_E_BOUNDS, "low >= high");
+      if (!(x.prior_sigma > 0))
+        return fail(h, TPE_E_INVALID, "hp " + std::to_string(i) + ": prior_sigma <= 0");
+    }
+    if (x.cond_count < 0 || x.cond_begin < 0 || x.cond_begin + x.cond_count > sp->n_cond)
+      return fail(h, TPE_E_INVALID, "hp " + std::to_string(i) + ": bad condition range");
+    for (int c = 0; c < x.cond_count; ++c) {
+      const int par = sp->cond_parent[x.cond_begin + c];
+      if (par < 0 || par >= sp->n_hp || par == i)
+        return fail(h, TPE_E_INVALID, "hp " + std::to_string(i) + ": bad condition parent");
+    }
+    if ((x.flags & TPE_PCHOICE) &&
+        (x.pprior_begin < 0 || x.pprior_begin + x.upper > sp->n_pprior))
+      return fail(h, TPE_E_INVALID, "hp " + std::to_string(i) + ": bad pchoice prior");
+  }
+  return TPE_OK;
+}
+
+// level(h) = 0 without conditions, else 1 + max(level(parent))
+int compute_levels(tpe_engine *h, tpe_plan *p) {
+  std::vector<int> lev(p->P, -1);
+  for (int iter = 0; iter <= p->P; ++iter) {
+    bool changed = false;
+    for (int i = 0; i < p->P; ++i) {
+      const tpe_hp &x = p->hps[i];
+      int l = 0;
+      bool ready = true;
+      for (int c = 0; c < x.cond_count; ++c) {
+        const int par = p->cond_parent[x.cond_begin + c];
+        if (lev[par] < 0) { ready = false; break; }
+        l = std::max(l, lev[par] + 1);
+      }
+      if (ready && lev[i] != l) { lev[i] = l; changed = true; }
+    }
+    if (!changed) break;
+  }
+  int nl = 0;
+  for (int i = 0; i < p->P; ++i) {
+    if (lev[i] < 0 || lev[i] > p->P) return fail(h, TPE_E_INVALID, "cyclic conditions");
+    nl = std::max(nl, lev[i] + 1);
+  }
+  p->levels.assign(nl, {});
+  for (int kind = 0; kind <= KIND_CAT; ++kind)
+    for (int i = 0; i < p->P; ++i)
+      if (score_kind(p->hps[i]) == kind) p->levels[lev[i]].push_back(i);
+  p->level_off.assign(nl + 1, 0);
+  p->groups.assign(nl, {});
+  for (int l = 0; l < nl; ++l) {
+    p->level_off[l + 1] = p->level_off[l] + (int)p->levels[l].size();
+    int j = 0;
+    const auto &L = p->levels[l];
+    while (j < (int)L.size()) {
+      const int kind = score_kind(p->hps[L[j]]);
+      int k = j;
+      while (k < (int)L.size() && score_kind(p->hps[L[k]]) == kind) ++k;
+      p->groups[l].push_back({kind, p->level_off[l] + j, k - j});
+      j = k;
+    }
+  }
+  return TPE_OK;
+}
+
+int plan_build(tpe_engine *h, const tpe_space *sp, int64_t max_trials, tpe_plan *p) {
+  int rc = validate_space(h, sp);
+  if (rc) return rc;
+  if (max_trials < 0) return fail(h, TPE_E_INVALID, "max_trials < 0");
+  p->eng = h;
+  p->P = sp->n_hp;
+  p->hps.assign(sp->hp, sp->hp + sp->n_hp);
+  p->cond_parent.assign(sp->cond_parent, sp->cond_parent + sp->n_cond);
+  p->cond_branch.assign(sp->cond_branch, sp->cond_branch + sp->n_cond);
+  p->pprior.assign(sp->pprior, sp->pprior + sp->n_pprior);
+  rc = compute_levels(h, p);
+  if (rc) return rc;
+  p->ncap = std::max<int64_t>(max_trials, 1);
+  int64_t kcap = p->ncap + 1;
+  for (const auto &x : p->hps)
+    if (x.family == TPE_CAT) kcap = std::max<int64_t>(kcap, x.upper);
+  p->kcap = kcap;
+  const int64_t slots = 2 * (int64_t)p->P;
+  CKH(hipSetDevice(h->device));
+  CKH(dalloc(&p->d_hps, p->P));
+  CKH(dalloc(&p->d_cp, p->cond_parent.size()));
+  CKH(dalloc(&p->d_cb, p->cond_branch.size()));
+  CKH(dalloc(&p->d_pprior, p->pprior.size()));
+  CKH(dalloc(&p->d_level_hps, p->P));
+  CKH(dalloc(&p->d_all_hps, p->P));
+  CKH(dalloc(&p->d_losses, p->ncap));
+  CKH(dalloc(&p->d_vals, (size_t)p->ncap * p->P));
+  CKH(dalloc(&p->d_active, (size_t)p->ncap * p->P));
+  CKH(dalloc(&p->d_below, p->ncap));
+  CKH(dalloc(&p->d_mw, (size_t)slots * kcap));
+  CKH(dalloc(&p->d_mmu, (size_t)slots * kcap));
+  CKH(dalloc(&p->d_msig, (size_t)slots * kcap));
+  CKH(dalloc(&p->d_scratch, (size_t)slots * kcap));
+  CKH(dalloc(&p->d_info, slots));
+  CKH(dalloc(&p->d_coef, (size_t)slots * kcap));
+  CKH(hipEventCreate(&p->ev0));
+  CKH(hipEventCreate(&p->ev1));
+  std::vector<int32_t> lh;
+  for (auto &l : p->levels) lh.insert(lh.end(), l.begin(), l.end());
+  std::vector<int32_t> all(p->P);
+  for (int i = 0; i < p->P; ++i) all[i] = i;
+  hipStream_t st = h->stream;
+  CKH(hipMemcpyAsync(p->d_hps, p->hps.data(), p->P * sizeof(tpe_hp), hipMemcpyHostToDevice, st));
+  if (!p->cond_parent.empty()) {
+    CKH(hipMemcpyAsync(p->d_cp, p->cond_parent.data(), p->cond_parent.size() * 4, hipMemcpyHostToDevice, st));
+    CKH(hipMemcpyAsync(p->d_cb, p->cond_branch.data(), p->cond_branch.size() * 4, hipMemcpyHostToDevice, st));
+  }
+  if (!p->pprior.empty())
+    CKH(hipMemcpyAsync(p->d_pprior, p->pprior.data(), p->pprior.size() * 8, hipMemcpyHostToDevice, st));
+  CKH(hipMemcpyAsync(p->d_level_hps, lh.data(), lh.size() * 4, hipMemcpyHostToDevice, st));
+  CKH(hipMemcpyAsync(p->d_all_hps, all.data(), all.size() * 4, hipMemcpyHostToDevice, st));
+  CKH(hipMemsetAsync(p->d_info, 0, slots * sizeof(MixInfo), st));
+  CKH(hipStreamSynchronize(st));
+  return TPE_OK;
+}
+
+int ensure_suggest_state(tpe_engine *h, tpe_plan *p, int64_t n_sug, size_t partials) {
+  if (n_sug > p->s_cap) {
+    dfree(p->d_results);
+    dfree(p->d_seeds);
+    p->d_results = nullptr;
+    p->d_seeds = nullptr;
+    CKH(dalloc(&p->d_results, (size_t)n_sug * p->P));
+    CKH(dalloc(&p->d_seeds, n_sug));
+    p->s_cap = n_sug;
+  }
+  if (partials > p->partial_cap) {
+    dfree(p->d_partial);
+    p->d_partial = nullptr;
+    CKH(dalloc(&p->d_partial, partials));
+    p->partial_cap = partials;
+  }
+  return TPE_OK;
+}
+
+int ensure_ext(tpe_engine *h, tpe_plan *p, size_t n) {
+  if (n > p->ext_cap) {
+    dfree(p->d_ext); dfree(p->d_lb); dfree(p->d_la);
+    p->d_ext = p->d_lb = p->d_la = nullptr;
+    CKH(dalloc(&p->d_ext, n));
+    CKH(dalloc(&p->d_lb, n));
+    CKH(dalloc(&p->d_la, n));
+    p->ext_cap = n;
+  }
+  return TPE_OK;
+}
+
+// component split + grid size for one level launch
+void choose_geometry(int64_t n_cand, int64_t n_slots, int64_t n_sug, int32_t &ks,
+                     int32_t &tiles, int32_t &grid_x) {
+  const int64_t target = 2048;  // ~8 workgroups per CU on 256 CUs
+  ks = 4;
+  for (int cand_ks : {1, 2, 4}) {
+    const int64_t tc = 64 * (4 / cand_ks);
+    const int64_t t = (n_cand + tc - 1) / tc;
+    if (t * n_slots * n_sug >= target || cand_ks == 4) { ks = cand_ks; break; }
+  }
+  const int64_t tc = 64 * (4 / ks);
+  tiles = (int32_t)std::max<int64_t>(0, (n_cand + tc - 1) / tc);
+  int64_t per = std::max<int64_t>(1, (target * 4) / std::max<int64_t>(1, n_slots * n_sug));
+  grid_x = (int32_t)std::max<int64_t>(1, std::min<int64_t>(std::max(tiles, 1), per));
+}
+
+int ensure_cand(tpe_engine *h, tpe_plan *p, size_t n) {
+  if (n > p->cand_cap) {
+    dfree(p->d_cand);
+    p->d_cand = nullptr;
+    CKH(dalloc(&p->d_cand, n));
+    p->cand_cap = n;
+  }
+  return TPE_OK;
+}
+
+// One (level, kind) group: draw candidates (unless external), score, reduce.
+// Candidates are processed in chunks so the buffer stays <= 512 MB.
+int run_group(tpe_engine *h, tpe_plan *p, int32_t kind, const int32_t *level_hps_dev,
+              int32_t n_slots, int64_t n_sug, int64_t n_cand, int64_t cand_begin,
+              const double *ext, double *lb, double *la, int32_t force, hipStream_t st) {
+  ScoreArgs a{};
+  a.hps = p->d_hps;
+  a.level_hps = level_hps_dev;
+  a.cond_parent = p->d_cp;
+  a.cond_branch = p->d_cb;
+  a.info = p->d_info;
+  a.coef = p->d_coef;
+  a.mw = p->d_mw;
+  a.mmu = p->d_mmu;
+  a.msig = p->d_msig;
+  a.seeds = p->d_seeds;
+  a.out_lb = lb;
+  a.out_la = la;
+  a.results = p->d_results;
+  a.kcap = p->kcap;
+  a.n_hp = p->P;
+  a.n_slots = n_slots;
+  a.n_suggest = (int32_t)n_sug;
+  a.force_active = force;
+  const int64_t budget = (int64_t)64 << 20;  // doubles
+  const int64_t chunk = ext ? std::max<int64_t>(n_cand, 1)
+                            : std::max<int64_t>(1, std::min<int64_t>(std::max<int64_t>(n_cand, 1),
+                                                   budget / std::max<int64_t>(1, n_sug * n_slots)));
+  int64_t c0 = 0;
+  do {
+    const int64_t cn = std::min(chunk, n_cand - c0);
+    int32_t ks, tiles, grid_x;
+    choose_geometry(cn, n_slots, n_sug, ks, tiles, grid_x);
+    int rc = ensure_suggest_state(h, p, n_sug, (size_t)n_sug * n_slots * grid_x);
+    if (rc) return rc;
+    a.partial = p->d_partial;
+    a.results = p->d_results;
+    a.seeds = p->d_seeds;
+    a.n_cand = cn;
+    a.cand_begin = cand_begin + c0;
+    a.ks = ks;
+    a.tiles = tiles;
+    if (ext) {
+      a.cand = ext;
+    } else {
+      rc = ensure_cand(h, p, (size_t)std::max<int64_t>(1, n_sug * n_slots * cn));
+      if (rc) return rc;
+      a.cand = p->d_cand;
+      CKH(launch_draw(a, st));
+    }
+    CKH(launch_score(a, kind, grid_x, st));
+    CKH(launch_reduce(level_hps_dev, n_slots, (int32_t)n_sug, p->P, grid_x, c0 > 0 ? 1 : 0,
+                      p->d_partial, p->d_results, st));
+    c0 += cn;
+  } while (c0 < n_cand);
+  return TPE_OK;
+}
+
+int copy_results(tpe_engine *h, tpe_plan *p, int64_t n_sug, tpe_result *out, int32_t on_dev,
+                 hipStream_t st) {
+  if (!out) return TPE_OK;
+  const size_t bytes = (size_t)n_sug * p->P * sizeof(tpe_result);
+  CKH(hipMemcpyAsync(out, p->d_results, bytes,
+                     on_dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, st));
+  if (!on_dev) CKH(hipStreamSynchronize(st));
+  return TPE_OK;
+}
+
+// one-hp operator plan cached in the engine
+int op_plan(tpe_engine *h, int32_t family, uint32_t flags, int32_t upper, double low,
+            double high, double q, int64_t ncap, tpe_plan **out) {
+  tpe_hp x{};
+  x.family = family;
+  x.flags = flags & (TPE_HAS_LOW | TPE_HAS_HIGH | TPE_HAS_Q);
+  x.obs_transform = TPE_OBS_IDENT;
+  x.upper = upper;
+  x.prior_mu = 0.0;
+  x.prior_sigma = 1.0;
+  x.low = low;
+  x.high = high;
+  x.q = q;
+  tpe_plan *p = h->op;
+  const int64_t need_k = std::max<int64_t>(ncap + 1, upper);
+  if (!p || p->ncap < ncap || p->kcap < need_k) {
+    if (p) { plan_free_buffers(p); delete p; h->op = nullptr; }
+    p = new tpe_plan();
+    tpe_space sp{};
+    sp.n_hp = 1;
+    sp.hp = &x;
+    x.upper = std::max<int32_t>(upper, 1);
+    const int64_t cap = std::max<int64_t>(ncap, 1024);
+    std::vector<double> pp_room((size_t)std::max<int64_t>(cap + 1, upper), 0.0);
+    sp.n_pprior = (int64_t)pp_room.size();
+    sp.pprior = pp_room.data();
+    int rc = plan_build(h, &sp, cap, p);
+    if (rc) { plan_free_buffers(p); delete p; return rc; }
+    h->op = p;
+  }
+  p->hps[0] = x;
+  CKH(hipMemcpyAsync(p->d_hps, &p->hps[0], sizeof(tpe_hp), hipMemcpyHostToDevice, h->stream));
+  *out = p;
+  return TPE_OK;
+}
+
+// upload an explicit mixture into slot `slot` of an operator plan
+int put_mixture(tpe_engine *h, tpe_plan *p, int slot, const double *w, const double *mu,
+                const double *sg, int64_t k, int32_t kind) {
+  hipStream_t st = h->stream;
+  CKH(hipMemcpyAsync(p->d_mw + slot * p->kcap, w, k * 8, hipMemcpyHostToDevice, st));
+  if (mu) CKH(hipMemcpyAsync(p->d_mmu + slot * p->kcap, mu, k * 8, hipMemcpyHostToDevice, st));
+  if (sg) CKH(hipMemcpyAsync(p->d_msig + slot * p->kcap, sg, k * 8, hipMemcpyHostToDevice, st));
+  MixInfo mi{};
+  mi.K = (int32_t)k;
+  mi.kind = kind;
+  CKH(hipMemcpyAsync(p->d_info + slot, &mi, sizeof(MixInfo), hipMemcpyHostToDevice, st));
+  CKH(hipStreamSynchronize(st));  // mi lives on this frame
+  return TPE_OK;
+}
+
+bool bad_family(int32_t f) { return f < TPE_GMM || f > TPE_CAT; }
+
+}  // namespace
+
+// ======================================================================
+// C ABI
+// ======================================================================
+extern "C" {
+
+const char *tpe_version(void) { return "tpe-mi355x 0.1 (gfx950)"; }
+
+int tpe_device_count(int32_t *n) {
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+  if (n) *n = c;
+  return TPE_OK;
+}
+
+int tpe_create(int32_t device, tpe_handle_t *out) {
+  if (!out) return TPE_E_INVALID;
+  *out = nullptr;
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess || c <= 0) return TPE_E_NODEVICE;
+  if (device < 0 || device >= c) return TPE_E_NODEVICE;
+  if (hipSetDevice(device) != hipSuccess) return TPE_E_HIP;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return TPE_E_HIP;
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return TPE_E_NODEVICE;
+  auto *h = new tpe_engine();
+  h->device = device;
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete h;
+    return TPE_E_HIP;
+  }
+  *out = h;
+  return TPE_OK;
+}
+
+int tpe_destroy(tpe_handle_t h) {
+  if (!h) return TPE_OK;
+  (void)hipSetDevice(h->device);
+  if (h->op) { plan_free_buffers(h->op); delete h->op; }
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+  return TPE_OK;
+}
+
+const char *tpe_last_error(tpe_handle_t h) { return h ? h->err.c_str() : "null handle"; }
+
+int tpe_synchronize(tpe_handle_t h) {
+  if (!h) return TPE_E_INVALID;
+  CKH(hipSetDevice(h->device));
+  CKH(hipDeviceSynchronize());
+  return TPE_OK;
+}
+
+int tpe_split(tpe_handle_t h, const double *losses, int64_t n, double gamma,
+              int32_t gamma_cap, uint8_t *below_mask) {
+  if (!h) return TPE_E_INVALID;
+  if (n < 0 || (n > 0 && (!losses || !below_mask))) return fail(h, TPE_E_INVALID, "bad args");
+  if (n == 0) return TPE_OK;
+  CKH(hipSetDevice(h->device));
+  tpe_plan *p;
+  int rc = op_plan(h, TPE_GMM, 0, 1, 0, 0, 0, n, &p);
+  if (rc) return rc;
+  const int32_t nb = (int32_t)std::min<double>(std::ceil(gamma * std::sqrt((double)n)), gamma_cap);
+  CKH(hipMemcpyAsync(p->d_losses, losses, n * 8, hipMemcpyHostToDevice, h->stream));
+  CKH(launch_split(p->d_losses, n, std::max(nb, 0), p->d_below, h->stream));
+  CKH(hipMemcpyAsync(below_mask, p->d_below, n, hipMemcpyDeviceToHost, h->stream));
+  CKH(hipStreamSynchronize(h->stream));
+  return TPE_OK;
+}
+
+static int fit_one(tpe_handle_t h, int32_t family, const double *obs, int64_t n,
+                   double prior_weight, double prior_mu, double prior_sigma, int32_t upper,
+                   const double *pprior, int32_t lf, tpe_plan **pout) {
+  tpe_plan *p;
+  int rc = op_plan(h, family, 0, upper, 0, 0, 0, n, &p);
+  if (rc) return rc;
+  p->hps[0].prior_mu = prior_mu;
+  p->hps[0].prior_sigma = prior_sigma;
+  p->hps[0].upper = upper;
+  if (pprior) {
+    p->hps[0].flags |= TPE_PCHOICE;
+    p->hps[0].pprior_begin = 0;
+    CKH(hipMemcpyAsync(p->d_pprior, pprior, upper * 8, hipMemcpyHostToDevice, h->stream));
+  }
+  CKH(hipMemcpyAsync(p->d_hps, &p->hps[0], sizeof(tpe_hp), hipMemcpyHostToDevice, h->stream));
+  if (n > 0) {
+    CKH(hipMemcpyAsync(p->d_vals, obs, n * 8, hipMemcpyHostToDevice, h->stream));
+    CKH(hipMemsetAsync(p->d_active, 1, n, h->stream));
+    CKH(hipMemsetAsync(p->d_below, 1, n, h->stream));
+  }
+  CKH(launch_fit(p->d_hps, 1, p->d_vals, p->d_active, p->d_below, n, prior_weight, lf, p->d_pprior,
+                 p->d_mw, p->d_mmu, p->d_msig, p->d_info, p->kcap, p->d_scratch, h->stream));
+  *pout = p;
+  return TPE_OK;
+}
+
+int tpe_parzen_fit(tpe_handle_t h, const double *obs, int64_t n, double prior_weight,
+                   double prior_mu, double prior_sigma, int32_t lf, double *w, double *mu,
+                   double *sigma) {
+  if (!h) return TPE_E_INVALID;
+  if (n < 0 || (n > 0 && !obs) || !w || !mu || !sigma) return fail(h, TPE_E_INVALID, "bad args");
+  if (!(prior_sigma > 0)) return fail(h, TPE_E_INVALID, "prior_sigma <= 0");
+  CKH(hipSetDevice(h->device));
+  tpe_plan *p;
+  int rc = fit_one(h, TPE_GMM, obs, n, prior_weight, prior_mu, prior_sigma, 1, nullptr, lf, &p);
+  if (rc) return rc;
+  const int64_t K = n + 1;
+  CKH(hipMemcpyAsync(w, p->d_mw, K * 8, hipMemcpyDeviceToHost, h->stream));
+  CKH(hipMemcpyAsync(mu, p->d_mmu, K * 8, hipMemcpyDeviceToHost, h->stream));
+  CKH(hipMemcpyAsync(sigma, p->d_msig, K * 8, hipMemcpyDeviceToHost, h->stream));
+  CKH(hipStreamSynchronize(h->stream));
+  return TPE_OK;
+}
+
+int tpe_categorical_posterior(tpe_handle_t h, const int64_t *obs, int64_t n, int32_t upper,
+                              double prior_weight, const double *pprior, int32_t lf,
+                              double *p_out) {
+  if (!h) return TPE_E_INVALID;
+  if (n < 0 || (n > 0 && !obs) || upper <= 0 || !p_out) return fail(h, TPE_E_INVALID, "bad args");
+  for (int64_t i = 0; i < n; ++i)
+    if (obs[i] < 0) return fail(h, TPE_E_INVALID, "negative categorical observation");
+  CKH(hipSetDevice(h->device));
+  std::vector<double> dv(obs, obs + n);
+  tpe_plan *p;
+  int rc = fit_one(h, TPE_CAT, dv.data(), n, prior_weight, 0, 1, upper, pprior, lf, &p);
+  if (rc) return rc;
+  CKH(hipMemcpyAsync(p_out, p->d_mw, upper * 8, hipMemcpyDeviceToHost, h->stream));
+  CKH(hipStreamSynchronize(h->stream));
+  return TPE_OK;
+}
+
+int tpe_score(tpe_handle_t h, int32_t family, const double *x, int64_t n, const double *wb,
+              const double *mb, const double *sb, int64_t kb, const double *wa, const double *ma,
+              const double *sa, int64_t ka, double low, double high, double q, uint32_t flags,
+              double *llik_b, double *llik_a, int64_t *best_index, double *best_score) {
+  if (!h) return TPE_E_INVALID;
+  if (bad_family(family) || n < 0 || kb <= 0 || ka <= 0 || !wb || !wa)
+    return fail(h, TPE_E_INVALID, "bad args");
+  if (family != TPE_CAT && (!mb || !sb || !ma || !sa)) return fail(h, TPE_E_INVALID, "bad args");
+  if (family == TPE_CAT && kb != ka) return fail(h, TPE_E_INVALID, "p length mismatch");
+  const bool hl = flags & TPE_HAS_LOW, hh = flags & TPE_HAS_HIGH;
+  if (family != TPE_CAT && (hl || hh)) {
+    if (hl != hh) return fail(h, TPE_E_INVALID, "one-sided truncation");
+    if (!(low < high)) return fail(h, TPE_E_BOUNDS, "low >= high");
+  }
+  if (best_index) *best_index = -1;
+  if (best_score) *best_score = NAN;
+  if (n == 0) return TPE_OK;
+  if (family == TPE_CAT) {
+    for (int64_t i = 0; i < n; ++i)
+      if (!(x[i] >= 0 && x[i] < kb && x[i] == std::floor(x[i])))
+        return fail(h, TPE_E_INDEX, "categorical sample out of range");
+  }
+  if (family == TPE_LGMM && (flags & TPE_HAS_Q)) {
+    const double hq = q / 2.0, eh = hh ? std::exp(high) : INFINITY;
+    for (int64_t i = 0; i < n; ++i) {
+      const double ub = std::min(x[i] + hq, eh);
+      if (ub < 0) return fail(h, TPE_E_NEGATIVE, "negative arg to lognormal_cdf");
+    }
+  }
+  CKH(hipSetDevice(h->device));
+  tpe_plan *p;
+  const int64_t kmax = std::max(kb, ka);
+  int rc = op_plan(h, family, flags, family == TPE_CAT ? (int32_t)kb : 1, low, high, q,
+                   std::max<int64_t>(kmax, 1), &p);
+  if (rc) return rc;
+  const int32_t kind = family == TPE_CAT ? 2 : ((flags & TPE_HAS_Q) ? 1 : 0);
+  rc = put_mixture(h, p, 0, wb, mb, sb, kb, kind);
+  if (rc) return rc;
+  rc = put_mixture(h, p, 1, wa, ma, sa, ka, kind);
+  if (rc) return rc;
+  CKH(launch_prep(p->d_hps, 1, p->d_mw, p->d_mmu, p->d_msig, p->d_info, p->d_coef, p->kcap,
+                  p->d_scratch, h->stream));
+  rc = ensure_ext(h, p, n);
+  if (rc) return rc;
+  CKH(hipMemcpyAsync(p->d_ext, x, n * 8, hipMemcpyHostToDevice, h->stream));
+  rc = run_group(h, p, score_kind(p->hps[0]), p->d_all_hps, 1, 1, n, 0, p->d_ext,
+                 llik_b ? p->d_lb : nullptr, llik_a ? p->d_la : nullptr, 1, h->stream);
+  if (rc) return rc;
+  tpe_result r;
+  CKH(hipMemcpyAsync(&r, p->d_results, sizeof(r), hipMemcpyDeviceToHost, h->stream));
+  if (llik_b) CKH(hipMemcpyAsync(llik_b, p->d_lb, n * 8, hipMemcpyDeviceToHost, h->stream));
+  if (llik_a) CKH(hipMemcpyAsync(llik_a, p->d_la, n * 8, hipMemcpyDeviceToHost, h->stream));
+  CKH(hipStreamSynchronize(h->stream));
+  if (best_index) *best_index = r.index;
+  if (best_score) *best_score = r.score;
+  return TPE_OK;
+}
+
+int tpe_lpdf(tpe_handle_t h, int32_t family, const double *x, int64_t n, const double *w,
+             const double *mu, const double *sigma, int64_t k, double low, double high, double q,
+             uint32_t flags, double *out) {
+  if (!out && n > 0) return fail(h, TPE_E_INVALID, "bad args");
+  return tpe_score(h, family, x, n, w, mu, sigma, k, w, mu, sigma, k, low, high, q, flags, out,
+                   nullptr, nullptr, nullptr);
+}
+
+int tpe_sample(tpe_handle_t h, int32_t family, const double *w, const double *mu,
+               const double *sigma, int64_t k, double low, double high, double q, uint32_t flags,
+               uint64_t seed, uint64_t stream, int64_t offset, int64_t n, double *out) {
+  if (!h) return TPE_E_INVALID;
+  if (bad_family(family) || k <= 0 || !w || n < 0 || (n > 0 && !out))
+    return fail(h, TPE_E_INVALID, "bad args");
+  if (family != TPE_CAT && (!mu || !sigma)) return fail(h, TPE_E_INVALID, "bad args");
+  const bool hl = flags & TPE_HAS_LOW, hh = flags & TPE_HAS_HIGH;
+  if (family != TPE_CAT && (hl || hh)) {
+    if (hl != hh) return fail(h, TPE_E_INVALID, "one-sided truncation");
+    if (!(low < high)) return fail(h, TPE_E_BOUNDS, "low >= high");
+  }
+  if (n == 0) return TPE_OK;
+  CKH(hipSetDevice(h->device));
+  tpe_plan *p;
+  int rc = op_plan(h, family, flags, family == TPE_CAT ? (int32_t)k : 1, low, high, q, k, &p);
+  if (rc) return rc;
+  const int32_t kind = family == TPE_CAT ? 2 : ((flags & TPE_HAS_Q) ? 1 : 0);
+  rc = put_mixture(h, p, 0, w, mu, sigma, k, kind);
+  if (rc) return rc;
+  rc = put_mixture(h, p, 1, w, mu, sigma, k, kind);
+  if (rc) return rc;
+  CKH(launch_prep(p->d_hps, 1, p->d_mw, p->d_mmu, p->d_msig, p->d_info, p->d_coef, p->kcap,
+                  p->d_scratch, h->stream));
+  rc = ensure_ext(h, p, n);
+  if (rc) return rc;
+  CKH(launch_sample(p->d_hps, p->d_mw, p->d_mmu, p->d_msig, p->d_info, seed, stream, offset, n,
+                    p->d_ext, h->stream));
+  CKH(hipMemcpyAsync(out, p->d_ext, n * 8, hipMemcpyDeviceToHost, h->stream));
+  CKH(hipStreamSynchronize(h->stream));
+  return TPE_OK;
+}
+
+// ---------------------------------------------------------------- plans
+int tpe_plan_create(tpe_handle_t h, const tpe_space *space, int64_t max_trials, tpe_plan_t *out) {
+  if (!h || !out) return TPE_E_INVALID;
+  *out = nullptr;
+  auto *p = new tpe_plan();
+  int rc = plan_build(h, space, max_trials, p);
+  if (rc) {
+    plan_free_buffers(p);
+    delete p;
+    return rc;
+  }
+  *out = p;
+  return TPE_OK;
+}
+
+int tpe_plan_destroy(tpe_plan_t p) {
+  if (!p) return TPE_OK;
+  (void)hipSetDevice(p->eng->device);
+  plan_free_buffers(p);
+  delete p;
+  return TPE_OK;
+}
+
+int tpe_plan_num_levels(tpe_plan_t p, int32_t *n) {
+  if (!p || !n) return TPE_E_INVALID;
+  *n = (int32_t)p->levels.size();
+  return TPE_OK;
+}
+
+int tpe_plan_set_history(tpe_plan_t p, const double *losses, const double *vals,
+                         const uint8_t *active, int64_t n, int32_t on_device, void *stream) {
+  if (!p) return TPE_E_INVALID;
+  tpe_engine *h = p->eng;
+  if (n < 0 || n > p->ncap) return fail(h, TPE_E_INVALID, "history larger than max_trials");
+  if (n > 0 && (!losses || !vals || !active)) return fail(h, TPE_E_INVALID, "bad args");
+  CKH(hipSetDevice(h->device));
+  hipStream_t st = pick_stream(h, stream);
+  const hipMemcpyKind kd = on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+  p->n = n;
+  if (n == 0) return TPE_OK;
+  CKH(hipMemcpyAsync(p->d_losses, losses, n * 8, kd, st));
+  CKH(hipMemcpyAsync(p->d_vals, vals, (size_t)n * p->P * 8, kd, st));
+  CKH(hipMemcpyAsync(p->d_active, active, (size_t)n * p->P, kd, st));
+  if (!on_device) CKH(hipStreamSynchronize(st));
+  return TPE_OK;
+}
+
+int tpe_plan_fit(tpe_plan_t p, double gamma, int32_t gamma_cap, double prior_weight, int32_t lf,
+                 void *stream) {
+  if (!p) return TPE_E_INVALID;
+  tpe_engine *h = p->eng;
+  CKH(hipSetDevice(h->device));
+  hipStream_t st = pick_stream(h, stream);
+  const double nbf = std::ceil(gamma * std::sqrt((double)p->n));
+  const int32_t nb = (int32_t)std::max(0.0, std::min<double>(nbf, gamma_cap));
+  if (p->n > 0) CKH(launch_split(p->d_losses, p->n, nb, p->d_below, st));
+  CKH(launch_fit(p->d_hps, p->P, p->d_vals, p->d_active, p->d_below, p->n, prior_weight, lf,
+                 p->d_pprior, p->d_mw, p->d_mmu, p->d_msig, p->d_info, p->kcap, p->d_scratch, st));
+  CKH(launch_prep(p->d_hps, p->P, p->d_mw, p->d_mmu, p->d_msig, p->d_info, p->d_coef, p->kcap,
+                  p->d_scratch, st));
+  return TPE_OK;
+}
+
+int tpe_plan_get_mixture(tpe_plan_t p, int32_t hp, int32_t side, double *w, double *mu,
+                         double *sigma, int64_t cap, int64_t *k) {
+  if (!p || !k) return TPE_E_INVALID;
+  tpe_engine *h = p->eng;
+  if (hp < 0 || hp >= p->P || side < 0 || side > 1) return fail(h, TPE_E_INVALID, "bad hp/side");
+  CKH(hipSetDevice(h->device));
+  CKH(hipDeviceSynchronize());
+  const int64_t slot = 2 * (int64_t)hp + side;
+  MixInfo mi;
+  CKH(hipMemcpy(&mi, p->d_info + slot, sizeof(mi), hipMemcpyDeviceToHost));
+  *k = mi.K;
+  if (mi.K > cap) return fail(h, TPE_E_INVALID, "capacity too small");
+  if (w) CKH(hipMemcpy(w, p->d_mw + slot * p->kcap, mi.K * 8, hipMemcpyDeviceToHost));
+  if (mu) CKH(hipMemcpy(mu, p->d_mmu + slot * p->kcap, mi.K * 8, hipMemcpyDeviceToHost));
+  if (sigma) CKH(hipMemcpy(sigma, p->d_msig + slot * p->kcap, mi.K * 8, hipMemcpyDeviceToHost));
+  return TPE_OK;
+}
+
+int tpe_plan_suggest(tpe_plan_t p, const uint64_t *seeds, int64_t n_sug, int64_t n_cand,
+                     int64_t cand_begin, int32_t level, tpe_result *out, int32_t out_on_device,
+                     void *stream) {
+  if (!p) return TPE_E_INVALID;
+  tpe_engine *h = p->eng;
+  if (n_sug <= 0 || n_cand < 0 || cand_begin < 0 || !seeds) return fail(h, TPE_E_INVALID, "bad args");
+  if (level >= (int32_t)p->levels.size()) return fail(h, TPE_E_INVALID, "bad level");
+  CKH(hipSetDevice(h->device));
+  hipStream_t st = pick_stream(h, stream);
+  int rc = ensure_suggest_state(h, p, n_sug, 1);
+  if (rc) return rc;
+  CKH(hipMemcpyAsync(p->d_seeds, seeds, n_sug * 8, hipMemcpyHostToDevice, st));
+  CKH(hipEventRecord(p->ev0, st));
+  const int l0 = level < 0 ? 0 : level;
+  const int l1 = level < 0 ? (int)p->levels.size() : level + 1;
+  for (int l = l0; l < l1; ++l)
+    for (const auto &g : p->groups[l]) {
+      rc = run_group(h, p, g.kind, p->d_level_hps + g.off, g.count, n_sug, n_cand, cand_begin,
+                     nullptr, nullptr, nullptr, 0, st);
+      if (rc) return rc;
+    }
+  CKH(hipEventRecord(p->ev1, st));
+  p->timed = true;
+  p->last_ncand = n_cand;
+  p->last_nsug = n_sug;
+  p->last_level = level;
+  return copy_results(h, p, n_sug, out, out_on_device, st);
+}
+
+int tpe_plan_merge(tpe_plan_t p, const tpe_result *gathered, int32_t world, int32_t level,
+                   tpe_result *out, int32_t out_on_device, void *stream) {
+  if (!p || !gathered || world <= 0) return TPE_E_INVALID;
+  tpe_engine *h = p->eng;
+  if (level < 0 || level >= (int32_t)p->levels.size()) return fail(h, TPE_E_INVALID, "bad level");
+  CKH(hipSetDevice(h->device));
+  hipStream_t st = pick_stream(h, stream);
+  const int32_t ns = (int32_t)p->levels[level].size();
+  CKH(launch_merge(p->d_level_hps + p->level_off[level], ns, (int32_t)p->last_nsug, p->P, world,
+                   reinterpret_cast<const Partial *>(gathered), p->d_results, st));
+  return copy_results(h, p, p->last_nsug, out, out_on_device, st);
+}
+
+int tpe_plan_score_candidates(tpe_plan_t p, int32_t hp, const double *x, int64_t n,
+                              double *llik_b, double *llik_a, int64_t *best_index,
+                              double *best_score) {
+  if (!p) return TPE_E_INVALID;
+  tpe_engine *h = p->eng;
+  if (hp < 0 || hp >= p->P || n < 0 || (n > 0 && !x)) return fail(h, TPE_E_INVALID, "bad args");
+  if (best_index) *best_index = -1;
+  if (best_score) *best_score = NAN;
+  if (n == 0) return TPE_OK;
+  const tpe_hp &H = p->hps[hp];
+  if (H.family == TPE_CAT) {
+    for (int64_t i = 0; i < n; ++i)
+      if (!(x[i] >= 0 && x[i] < H.upper && x[i] == std::floor(x[i])))
+        return fail(h, TPE_E_INDEX, "categorical sample out of range");
+  }
+  CKH(hipSetDevice(h->device));
+  hipStream_t st = h->stream;
+  CKH(hipDeviceSynchronize());
+  int rc = ensure_ext(h, p, n);
+  if (rc) return rc;
+  CKH(hipMemcpyAsync(p->d_ext, x, n * 8, hipMemcpyHostToDevice, st));
+  rc = run_group(h, p, score_kind(H), p->d_all_hps + hp, 1, 1, n, 0, p->d_ext,
+                 llik_b ? p->d_lb : nullptr, llik_a ? p->d_la : nullptr, 1, st);
+  if (rc) return rc;
+  tpe_result r;
+  CKH(hipMemcpyAsync(&r, p->d_results + hp, sizeof(r), hipMemcpyDeviceToHost, st));
+  if (llik_b) CKH(hipMemcpyAsync(llik_b, p->d_lb, n * 8, hipMemcpyDeviceToHost, st));
+  if (llik_a) CKH(hipMemcpyAsync(llik_a, p->d_la, n * 8, hipMemcpyDeviceToHost, st));
+  CKH(hipStreamSynchronize(st));
+  if (best_index) *best_index = r.index;
+  if (best_score) *best_score = r.score;
+  return TPE_OK;
+}
+
+int tpe_plan_last_stats(tpe_plan_t p, double *score_ms, double *pairs) {
+  if (!p) return TPE_E_INVALID;
+  tpe_engine *h = p->eng;
+  if (!p->timed) return fail(h, TPE_E_INVALID, "no suggest recorded");
+  CKH(hipSetDevice(h->device));
+  CKH(hipEventSynchronize(p->ev1));
+  float ms = 0.f;
+  CKH(hipEventElapsedTime(&ms, p->ev0, p->ev1));
+  if (score_ms) *score_ms = ms;
+  if (pairs) {
+    std::vector<MixInfo> info(2 * (size_t)p->P);
+    std::vector<Partial> res((size_t)p->last_nsug * p->P);
+    CKH(hipMemcpy(info.data(), p->d_info, info.size() * sizeof(MixInfo), hipMemcpyDeviceToHost));
+    CKH(hipMemcpy(res.data(), p->d_results, res.size() * sizeof(Partial), hipMemcpyDeviceToHost));
+    const int l0 = p->last_level < 0 ? 0 : p->last_level;
+    const int l1 = p->last_level < 0 ? (int)p->levels.size() : p->last_level + 1;
+    double acc = 0;
+    for (int l = l0; l < l1; ++l)
+      for (int hp : p->levels[l]) {
+        if (p->hps[hp].family == TPE_CAT) continue;
+        const double kk = (double)info[2 * hp].K + info[2 * hp + 1].K;
+        for (int64_t s = 0; s < p->last_nsug; ++s)
+          if (res[s * p->P + hp].active) acc += kk * (double)p->last_ncand;
+      }
+    *pairs = acc;
+  }
+  return TPE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,104 @@
+// tpe_internal.hpp -- shared host/device declarations of the TPE engine.
+// Not part of the ABI (include/tpe_engine.h is).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/tpe_engine.h"
+
+namespace tpe {
+
+constexpr double kEPS = 1e-12;  // hyperopt/tpe.py:25
+constexpr int kFitThreads = 1024;
+constexpr int kScoreThreads = 256;
+constexpr int kMaxLeaves = 160;  // numpy pairwise leaves per 8192 chunk (<=128)
+
+// Per (hp, side) mixture slot, written by k_fit / k_prep.
+// scoring kernel instantiations (lpdf kinds)
+enum { KIND_LSE_G = 0, KIND_LSE_L = 1, KIND_ERF_G = 2, KIND_ERF_L = 3, KIND_CAT = 4 };
+
+__host__ __device__ inline int score_kind(const tpe_hp &h) {
+  if (h.family == TPE_CAT) return KIND_CAT;
+  const bool lg = h.family == TPE_LGMM;
+  if (h.flags & TPE_HAS_Q) return lg ? KIND_ERF_L : KIND_ERF_G;
+  return lg ? KIND_LSE_L : KIND_LSE_G;
+}
+
+struct MixInfo {
+  int32_t K;        // components (categorical: upper)
+  int32_t kind;     // 0 LSE, 1 ERF, 2 CAT
+  double p_accept;  // truncation mass (tpe.py:130-136, 273-276)
+  double log_pacc;  // log(p_accept) subtracted by the quantized lpdf
+  double wsum;      // sum of weights (sampler CDF total)
+};
+
+// Per-component scoring coefficients, 32 B (one s_load_dwordx8).
+//   LSE: x = mu, y = a (sqrt(.5 log2 e)/max(sigma,EPS)), z = c (log2 units)
+//   ERF: x = mu, y = 1/max(sqrt2*sigma, EPS), z = w
+//   CAT: x = log p
+struct __attribute__((aligned(32))) Coef {
+  double x, y, z, w;
+};
+
+struct Partial {  // == tpe_result layout
+  double score;
+  double value;
+  int64_t index;
+  int32_t active;
+  int32_t pad;
+};
+static_assert(sizeof(Partial) == sizeof(tpe_result), "layout");
+
+struct ScoreArgs {
+  const tpe_hp *hps;
+  const int32_t *level_hps;  // hp ids of this launch (blockIdx.y)
+  const int32_t *cond_parent;
+  const int32_t *cond_branch;
+  const MixInfo *info;       // [2*P]
+  const Coef *coef;          // [2*P][kcap]
+  const double *mw, *mmu, *msig;  // [2*P][kcap] (sampler reads side 0)
+  const uint64_t *seeds;     // [S]
+  const double *cand;        // candidates [S][n_slots][n_cand] (drawn or external)
+  double *out_lb, *out_la;   // optional per-candidate lliks (ext only)
+  Partial *results;          // [S][P]
+  Partial *partial;          // [S][n_slots][grid.x]
+  int64_t kcap;
+  int64_t n_cand;
+  int64_t cand_begin;
+  int32_t n_hp;
+  int32_t n_slots;
+  int32_t ks;                // component split across the 4 waves (1,2,4)
+  int32_t tiles;             // candidate tiles per (s, hp)
+  int32_t n_suggest;         // grid.z
+  int32_t force_active;      // ignore conditions (operator-level scoring)
+};
+
+// ---- launch wrappers (tpe_kernels.hip) ----
+hipError_t launch_split(const double *losses, int64_t n, int32_t n_below,
+                        uint8_t *below, hipStream_t st);
+hipError_t launch_fit(const tpe_hp *hps, int32_t n_hp, const double *vals,
+                      const uint8_t *active, const uint8_t *below, int64_t n,
+                      double prior_weight, int32_t lf, const double *pprior,
+                      double *mw, double *mmu, double *msig, MixInfo *info,
+                      int64_t kcap, double *scratch, hipStream_t st);
+hipError_t launch_prep(const tpe_hp *hps, int32_t n_hp, const double *mw,
+                       const double *mmu, const double *msig, MixInfo *info,
+                       Coef *coef, int64_t kcap, double *scratch,
+                       hipStream_t st);
+hipError_t launch_score(const ScoreArgs &a, int32_t kind, int32_t grid_x, hipStream_t st);
+hipError_t launch_draw(const ScoreArgs &a, hipStream_t st);
+hipError_t launch_reduce(const int32_t *level_hps, int32_t n_slots,
+                         int32_t n_suggest, int32_t n_hp, int32_t grid_x,
+                         int32_t accumulate, const Partial *partial,
+                         Partial *results, hipStream_t st);
+hipError_t launch_merge(const int32_t *level_hps, int32_t n_slots,
+                        int32_t n_suggest, int32_t n_hp, int32_t world,
+                        const Partial *gathered, Partial *results,
+                        hipStream_t st);
+hipError_t launch_sample(const tpe_hp *hp_dev, const double *mw,
+                         const double *mmu, const double *msig,
+                         const MixInfo *info, uint64_t seed, uint64_t stream,
+                         int64_t offset, int64_t n, double *out,
+                         hipStream_t st);
+
+}  // namespace tpe

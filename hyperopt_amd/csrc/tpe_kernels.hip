@@ -1,0 +1,928 @@
+// tpe_kernels.hip -- hand-written CDNA4 (gfx950) kernels of the TPE hot path.
+//
+// Reference semantics (pminervini/hyperopt, hyperopt/tpe.py):
+//   k_split   : ap_filter_trials loss ranking            tpe.py:613-641
+//   k_fit     : adaptive_parzen_normal / categorical      tpe.py:381-475, 573-607
+//   k_prep    : GMM1_lpdf / LGMM1_lpdf per-component      tpe.py:104-166, 259-301
+//               constants, truncation mass p_accept
+//   k_score   : candidate draw (GMM1/LGMM1/categorical,   tpe.py:62-93, 216-250
+//               counter-based Philox in registers), below/above lpdf
+//               (log-sum-exp or linear erf-CDF sum), EI and block argmax
+//                                                         tpe.py:684-698, 749-759
+//   k_reduce / k_merge : grid / cross-device argmax with numpy semantics
+//
+// Layout: one 64-lane wave owns 64 candidates; mixture components are read
+// with wave-uniform addresses (scalar loads -> SGPR operands), so no LDS or
+// VGPRs are spent on them and HBM traffic per pair is ~0.
+#include <math.h>
+
+#include <algorithm>
+
+#include "tpe_internal.hpp"
+
+namespace tpe {
+
+// ------------------------------------------------------------------------
+// numpy-compatible scalar helpers
+// ------------------------------------------------------------------------
+__device__ __forceinline__ double np_maximum(double a, double b) {
+  if (a != a) return a;
+  if (b != b) return b;
+  return a >= b ? a : b;
+}
+__device__ __forceinline__ double np_minimum(double a, double b) {
+  if (a != a) return a;
+  if (b != b) return b;
+  return a <= b ? a : b;
+}
+
+// numpy float64 sum (np.sum / ndarray.sum): the reduction runs over buffers
+// of 8192 elements; each buffer is summed by numpy's pairwise_sum (blocks of
+// <= 128 with 8 accumulators, split at n/2 rounded down to a multiple of 8).
+// Reproducing it keeps the Parzen weights and p_accept bit-identical.
+__device__ double np_leaf_sum(const double *a, int n) {
+#pragma clang fp contract(off)
+  if (n < 8) {
+    double r = 0.0;
+    for (int i = 0; i < n; ++i) r += a[i];
+    return r;
+  }
+  double r0 = a[0], r1 = a[1], r2 = a[2], r3 = a[3], r4 = a[4], r5 = a[5],
+         r6 = a[6], r7 = a[7];
+  int i = 8;
+  for (; i < n - (n % 8); i += 8) {
+    r0 += a[i + 0]; r1 += a[i + 1]; r2 += a[i + 2]; r3 += a[i + 3];
+    r4 += a[i + 4]; r5 += a[i + 5]; r6 += a[i + 6]; r7 += a[i + 7];
+  }
+  double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+  for (; i < n; ++i) res += a[i];
+  return res;
+}
+
+template <int D>
+__device__ void np_leaves(int off, int n, int *lo, int *ln, int &cnt) {
+  if (n <= 128) { lo[cnt] = off; ln[cnt] = n; ++cnt; return; }
+  int n2 = n / 2;
+  n2 -= n2 % 8;
+  np_leaves<D - 1>(off, n2, lo, ln, cnt);
+  np_leaves<D - 1>(off + n2, n - n2, lo, ln, cnt);
+}
+template <>
+__device__ void np_leaves<0>(int off, int n, int *lo, int *ln, int &cnt) {
+  lo[cnt] = off; ln[cnt] = n; ++cnt;
+}
+template <int D>
+__device__ double np_combine(int n, const double *leaf, int &idx) {
+  if (n <= 128) return leaf[idx++];
+  int n2 = n / 2;
+  n2 -= n2 % 8;
+  const double a = np_combine<D - 1>(n2, leaf, idx);
+  const double b = np_combine<D - 1>(n - n2, leaf, idx);
+  return a + b;
+}
+template <>
+__device__ double np_combine<0>(int n, const double *leaf, int &idx) {
+  return leaf[idx++];
+}
+
+// Block-cooperative np.sum of a[0..n) (a in global memory, written by this
+// block before the call and visible after __syncthreads()).
+struct NpSumSmem {
+  int lo[kMaxLeaves];
+  int ln[kMaxLeaves];
+  double leaf[kMaxLeaves];
+  int cnt;
+  double total;
+};
+__device__ double block_np_sum(const double *a, int64_t n, NpSumSmem &sm) {
+#pragma clang fp contract(off)
+  double total = 0.0;
+  for (int64_t c0 = 0; c0 < n; c0 += 8192) {
+    const int cn = (int)min<int64_t>(8192, n - c0);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int cnt = 0;
+      np_leaves<8>(0, cn, sm.lo, sm.ln, cnt);
+      sm.cnt = cnt;
+    }
+    __syncthreads();
+    for (int l = threadIdx.x; l < sm.cnt; l += blockDim.x)
+      sm.leaf[l] = np_leaf_sum(a + c0 + sm.lo[l], sm.ln[l]);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int idx = 0;
+      const double part = np_combine<8>(cn, sm.leaf, idx);
+      sm.total = (c0 == 0) ? (0.0 + part) : (sm.total + part);
+    }
+  }
+  __syncthreads();
+  if (n > 0) total = sm.total;
+  __syncthreads();
+  return total;
+}
+
+// Block-wide exclusive scan of small ints (blockDim multiple of 64).
+__device__ int block_excl_scan(int v, int *wsum, int &total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nw = blockDim.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[wid] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int w = 0; w < nw; ++w) {
+      const int t = wsum[w];
+      wsum[w] = acc;
+      acc += t;
+    }
+    wsum[nw] = acc;
+  }
+  __syncthreads();
+  const int res = wsum[wid] + x - v;
+  total = wsum[nw];
+  __syncthreads();
+  return res;
+}
+
+template <typename T>
+__device__ T block_sum_i(T v, T *buf) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if (lane == 0) buf[wid] = v;
+  __syncthreads();
+  T t = 0;
+  if (threadIdx.x == 0) {
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += buf[w];
+    buf[0] = t;
+  }
+  __syncthreads();
+  t = buf[0];
+  __syncthreads();
+  return t;
+}
+
+// ------------------------------------------------------------------------
+// (a2) split: mark the n_below lowest losses.  Key order = numpy argsort with
+// NaN last; ties by position (stable).  One block, n_below <= 25 rounds of a
+// block-wide argmin (top-k with k <= 25).
+// ------------------------------------------------------------------------
+__device__ __forceinline__ bool key_less(double a, int64_t ia, double b,
+                                         int64_t ib) {
+  const bool na = a != a, nb = b != b;
+  if (na != nb) return nb;  // non-NaN before NaN
+  if (!na && a != b) return a < b;
+  return ia < ib;
+}
+
+__global__ __launch_bounds__(1024) void k_split(const double *__restrict__ losses,
+                                                int64_t n, int32_t n_below,
+                                                uint8_t *__restrict__ below) {
+  __shared__ double sv[16];
+  __shared__ int64_t si[16];
+  for (int64_t j = threadIdx.x; j < n; j += blockDim.x) below[j] = 0;
+  __syncthreads();
+  // previous winner (strict lower bound of remaining keys)
+  double pv = -INFINITY;
+  int64_t pi = -1;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int r = 0; r < n_below && r < n; ++r) {
+    double bv = NAN;
+    int64_t bi = -1;
+    for (int64_t j = threadIdx.x; j < n; j += blockDim.x) {
+      const double v = losses[j];
+      if (pi >= 0 && !key_less(pv, pi, v, j)) continue;  // already taken
+      if (bi < 0 || key_less(v, j, bv, bi)) { bv = v; bi = j; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double ov = __shfl_xor(bv, o, 64);
+      const int64_t oi = __shfl_xor(bi, o, 64);
+      if (oi >= 0 && (bi < 0 || key_less(ov, oi, bv, bi))) { bv = ov; bi = oi; }
+    }
+    if (lane == 0) { sv[wid] = bv; si[wid] = bi; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int w = 1; w < (int)(blockDim.x >> 6); ++w)
+        if (si[w] >= 0 && (bi < 0 || key_less(sv[w], si[w], bv, bi))) {
+          bv = sv[w]; bi = si[w];
+        }
+      sv[0] = bv; si[0] = bi;
+      if (bi >= 0) below[bi] = 1;
+    }
+    __syncthreads();
+    pv = sv[0]; pi = si[0];
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------
+// (a3)/(a4)/(a8) Parzen fit / categorical posterior, one block per (hp, side)
+// ------------------------------------------------------------------------
+// linear_forgetting_weights(n, lf)[i], tpe.py:381-394, with numpy linspace
+// rounding (i*step + start; last element == stop).
+__device__ __forceinline__ double lf_weight(int64_t i, int64_t n, int32_t lf) {
+#pragma clang fp contract(off)
+  if (n < lf) return 1.0;
+  const int64_t m = n - lf;  // ramp length
+  if (i >= m) return 1.0;
+  const double start = 1.0 / (double)n;
+  if (m == 1) return start;
+  if (i == m - 1) return 1.0;
+  const double step = (1.0 - start) / (double)(m - 1);
+  return (double)i * step + start;
+}
+
+__device__ __forceinline__ double obs_transform(double v, int32_t tf, double low) {
+  switch (tf) {
+    case TPE_OBS_LOG: return log(v);
+    case TPE_OBS_LOG_CLIP_EXPLOW: return log(np_maximum(v, np_maximum(kEPS, exp(low))));
+    case TPE_OBS_LOG_CLIP_EPS: return log(np_maximum(v, kEPS));
+    default: return v;
+  }
+}
+
+// rank of element i in a stable ascending sort with NaN last
+__device__ __forceinline__ bool before(double vj, int64_t j, double vi, int64_t i) {
+  if (vi != vi) return (vj == vj) || j < i;
+  return vj < vi || (vj == vi && j < i);
+}
+
+struct FitSmem {
+  int wsum[17];
+  int64_t cnt64[16];
+  NpSumSmem np;
+};
+
+__global__ __launch_bounds__(1024) void k_fit(
+    const tpe_hp *__restrict__ hps, const double *__restrict__ vals,
+    const uint8_t *__restrict__ active, const uint8_t *__restrict__ below,
+    int64_t n, double prior_weight, int32_t lf, const double *__restrict__ pprior,
+    double *__restrict__ mw, double *__restrict__ mmu, double *__restrict__ msig,
+    MixInfo *__restrict__ info, int64_t kcap, double *__restrict__ scratch) {
+#pragma clang fp contract(off)
+  extern __shared__ __attribute__((aligned(16))) double dyn_lds[];
+  __shared__ FitSmem sm;
+  const int hp = blockIdx.x, side = blockIdx.y;  // side 0 = below ("good")
+  const int64_t slot = 2 * (int64_t)hp + side;
+  const tpe_hp H = hps[hp];
+  double *w = mw + slot * kcap;
+  double *mu = mmu + slot * kcap;
+  double *sg = msig + slot * kcap;
+  double *ob = scratch + slot * kcap;  // observations in tid order
+  const double *row = vals + (int64_t)hp * n;
+  const uint8_t *arow = active + (int64_t)hp * n;
+  const uint8_t want = side == 0 ? 1 : 0;
+
+  // ---- gather this side's observations, keeping tid order (tpe.py:629-636)
+  int m = 0;
+  for (int64_t c0 = 0; c0 < n; c0 += blockDim.x) {
+    const int64_t j = c0 + threadIdx.x;
+    const int f = (j < n && arow[j] && below[j] == want) ? 1 : 0;
+    int tot;
+    const int pos = block_excl_scan(f, sm.wsum, tot);
+    if (f) ob[m + pos] = obs_transform(row[j], H.obs_transform, H.low);
+    m += tot;
+  }
+  __syncthreads();
+  // cache in LDS when it fits (dynamic size chosen by the launcher)
+  double *sob = dyn_lds;
+  const bool use_lds = (int64_t)m * 8 <= (int64_t)(96 * 1024);
+  if (use_lds) {
+    for (int i = threadIdx.x; i < m; i += blockDim.x) sob[i] = ob[i];
+    __syncthreads();
+  } else {
+    sob = ob;
+  }
+
+  if (H.family == TPE_CAT) {
+    // LF-weighted bincount in observation order (np.bincount) + pseudocounts
+    const int upper = H.upper;
+    for (int c = threadIdx.x; c < upper; c += blockDim.x) {
+      double cnt = 0.0;
+      for (int i = 0; i < m; ++i)
+        if ((int64_t)sob[i] == c) cnt += lf_weight(i, m, lf);
+      double pc;
+      if (H.flags & TPE_PCHOICE)
+        pc = cnt + (double)upper * (prior_weight * pprior[H.pprior_begin + c]);
+      else
+        pc = cnt + prior_weight;
+      w[c] = pc;
+    }
+    __syncthreads();
+    const double tot = block_np_sum(w, upper, sm.np);
+    for (int c = threadIdx.x; c < upper; c += blockDim.x) {
+      w[c] = w[c] / tot;
+      mu[c] = 0.0;
+      sg[c] = 0.0;
+    }
+    if (threadIdx.x == 0) { info[slot].K = upper; info[slot].kind = 2; }
+    return;
+  }
+
+  const double pm = H.prior_mu, ps = H.prior_sigma;
+  int pos = 0;
+  if (m == 0) {  // tpe.py:410-413
+    if (threadIdx.x == 0) { mu[0] = pm; sg[0] = ps; w[0] = prior_weight; }
+  } else if (m == 1) {  // tpe.py:414-422
+    if (threadIdx.x == 0) {
+      const double o = sob[0];
+      if (pm < o) {
+        pos = 0; mu[0] = pm; mu[1] = o; sg[0] = ps; sg[1] = ps * .5;
+      } else {
+        pos = 1; mu[0] = o; mu[1] = pm; sg[0] = ps * .5; sg[1] = ps;
+      }
+      w[0] = 1.0; w[1] = 1.0; w[pos] = prior_weight;
+    }
+  } else {  // tpe.py:423-454
+    // prior_pos = searchsorted(sorted, prior_mu, 'left') = #{obs < pm}
+    int cl = 0;
+    for (int i = threadIdx.x; i < m; i += blockDim.x) cl += (sob[i] < pm) ? 1 : 0;
+    pos = block_sum_i<int>(cl, sm.wsum);
+    const bool lfw = lf && lf < m;
+    // rank by counting (stable; 4 elements per pass share each LDS read)
+    for (int i0 = threadIdx.x; i0 < m; i0 += 4 * blockDim.x) {
+      int idx[4];
+      double vi[4];
+      int rk[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        idx[u] = i0 + u * (int)blockDim.x;
+        vi[u] = idx[u] < m ? sob[idx[u]] : 0.0;
+        rk[u] = 0;
+      }
+      for (int j = 0; j < m; ++j) {
+        const double vj = sob[j];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) rk[u] += before(vj, j, vi[u], idx[u]) ? 1 : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (idx[u] < m) {
+          const int r = rk[u] + (rk[u] >= pos ? 1 : 0);
+          mu[r] = vi[u];
+          w[r] = lfw ? lf_weight(idx[u], m, lf) : 1.0;
+        }
+      }
+    }
+    if (threadIdx.x == 0) { mu[pos] = pm; w[pos] = prior_weight; }
+    __syncthreads();
+    const int K = m + 1;
+    for (int k = threadIdx.x; k < K; k += blockDim.x) {
+      double s;
+      if (k == 0) s = mu[1] - mu[0];
+      else if (k == K - 1) s = mu[K - 1] - mu[K - 2];
+      else s = np_maximum(mu[k] - mu[k - 1], mu[k + 1] - mu[k]);
+      sg[k] = s;
+    }
+  }
+  __syncthreads();
+  const int K = m + 1;
+  // clip (tpe.py:456-462): prior_sigma / min(100, 1 + K)
+  const double hi = ps / 1.0;
+  const double lo = ps / fmin(100.0, 1.0 + (double)K);
+  for (int k = threadIdx.x; k < K; k += blockDim.x)
+    sg[k] = np_minimum(np_maximum(sg[k], lo), hi);
+  __syncthreads();
+  if (threadIdx.x == 0) sg[pos] = ps;
+  __syncthreads();
+  const double tot = block_np_sum(w, K, sm.np);
+  for (int k = threadIdx.x; k < K; k += blockDim.x) w[k] = w[k] / tot;
+  if (threadIdx.x == 0) { info[slot].K = K; info[slot].kind = 0; }
+}
+
+// ------------------------------------------------------------------------
+// per-component lpdf constants + p_accept, one block per (hp, side)
+// ------------------------------------------------------------------------
+__device__ __forceinline__ double normal_cdf(double x, double mu, double sigma) {
+#pragma clang fp contract(off)
+  const double bottom = np_maximum(1.4142135623730951 * sigma, kEPS);
+  const double z = (x - mu) / bottom;
+  return 0.5 * (1.0 + erf(z));
+}
+
+__global__ __launch_bounds__(256) void k_prep(
+    const tpe_hp *__restrict__ hps, const double *__restrict__ mw,
+    const double *__restrict__ mmu, const double *__restrict__ msig,
+    MixInfo *__restrict__ info, Coef *__restrict__ coef, int64_t kcap,
+    double *__restrict__ scratch) {
+#pragma clang fp contract(off)
+  __shared__ NpSumSmem np;
+  const int hp = blockIdx.x, side = blockIdx.y;
+  const int64_t slot = 2 * (int64_t)hp + side;
+  const tpe_hp H = hps[hp];
+  const int K = info[slot].K;
+  const double *w = mw + slot * kcap;
+  const double *mu = mmu + slot * kcap;
+  const double *sg = msig + slot * kcap;
+  Coef *cf = coef + slot * kcap;
+  double *tmp = scratch + slot * kcap;
+  const double wsum = block_np_sum(w, K, np);
+  if (H.family == TPE_CAT) {
+    for (int k = threadIdx.x; k < K; k += blockDim.x) {
+      Coef c; c.x = log(w[k]); c.y = 0.0; c.z = 0.0; c.w = 0.0;
+      cf[k] = c;
+    }
+    if (threadIdx.x == 0) {
+      info[slot].kind = 2; info[slot].p_accept = 1.0; info[slot].log_pacc = 0.0;
+      info[slot].wsum = wsum;
+    }
+    return;
+  }
+  const bool bounded = (H.flags & (TPE_HAS_LOW | TPE_HAS_HIGH)) != 0;
+  double pacc = 1.0;
+  if (bounded) {  // tpe.py:130-136 / 273-276 (log-space bounds for LGMM)
+    for (int k = threadIdx.x; k < K; k += blockDim.x)
+      tmp[k] = w[k] * (normal_cdf(H.high, mu[k], sg[k]) - normal_cdf(H.low, mu[k], sg[k]));
+    __syncthreads();
+    pacc = block_np_sum(tmp, K, np);
+  }
+  const bool quant = (H.flags & TPE_HAS_Q) != 0;
+  const double L2E = 1.4426950408889634;  // log2(e)
+  const double A0 = sqrt(0.5 * L2E);
+  for (int k = threadIdx.x; k < K; k += blockDim.x) {
+    Coef c;
+    const double s = sg[k];
+    const double sp = np_maximum(s, kEPS);
+    c.x = mu[k];
+    c.w = 0.0;
+    if (quant) {
+      c.y = 1.0 / np_maximum(1.4142135623730951 * s, kEPS);
+      c.z = w[k];
+    } else if (H.family == TPE_GMM) {
+      // log(w / sqrt(2 pi sigma^2) / p_accept), tpe.py:140-144
+      const double Z = sqrt(2.0 * 3.141592653589793 * (s * s));
+      c.y = A0 / sp;
+      c.z = L2E * log(w[k] / Z / pacc);
+    } else {
+      // lognormal_lpdf + log w, minus log(x) per candidate, tpe.py:193-202, 280
+      c.y = A0 / sp;
+      c.z = L2E * (log(w[k]) - log(sp * 2.5066282746310002));
+    }
+    cf[k] = c;
+  }
+  if (threadIdx.x == 0) {
+    info[slot].kind = quant ? 1 : 0;
+    info[slot].p_accept = pacc;
+    info[slot].log_pacc = log(pacc);
+    info[slot].wsum = wsum;
+  }
+}
+
+// ------------------------------------------------------------------------
+// counter-based Philox4x32-10 in registers
+// ------------------------------------------------------------------------
+struct U4 { uint32_t x, y, z, w; };
+__device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+__device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
+  return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
+}
+
+struct Draw { double u0, u1, u2, u3; };
+__device__ __forceinline__ Draw draw4(uint64_t seed, uint64_t gi, uint32_t stream,
+                                      uint32_t it) {
+  const U4 c0{(uint32_t)gi, (uint32_t)(gi >> 32), stream, 2u * it};
+  const U4 c1{(uint32_t)gi, (uint32_t)(gi >> 32), stream, 2u * it + 1u};
+  const U4 r0 = philox(c0, (uint32_t)seed, (uint32_t)(seed >> 32));
+  const U4 r1 = philox(c1, (uint32_t)seed, (uint32_t)(seed >> 32));
+  return Draw{u53(r0.x, r0.y), u53(r0.z, r0.w), u53(r1.x, r1.y), u53(r1.z, r1.w)};
+}
+
+// inverse CDF pick of a component with probability w[k] / wsum
+__device__ __forceinline__ int pick(const double *__restrict__ w, int K, double t) {
+  int k = 0;
+  double acc = w[0];
+  while (k < K - 1 && acc <= t) { ++k; acc += w[k]; }
+  return k;
+}
+
+// One GMM1/LGMM1/categorical draw (tpe.py:62-93, 216-250; stochastic.py:104)
+__device__ double draw_one(const tpe_hp &H, const MixInfo &I,
+                           const double *__restrict__ w,
+                           const double *__restrict__ mu,
+                           const double *__restrict__ sg, uint64_t seed,
+                           uint64_t gi, uint32_t stream) {
+  if (H.family == TPE_CAT) {
+    const Draw d = draw4(seed, gi, stream, 0);
+    return (double)pick(w, I.K, d.u0 * I.wsum);
+  }
+  const bool bounded = (H.flags & (TPE_HAS_LOW | TPE_HAS_HIGH)) != 0;
+  double x = 0.0;
+  bool ok = false;
+  int k = 0;
+  Draw d{};
+  for (uint32_t it = 0; it < 64 && !ok; ++it) {
+    d = draw4(seed, gi, stream, it);
+    k = pick(w, I.K, d.u0 * I.wsum);
+    const double z = sqrt(-2.0 * log(1.0 - d.u1)) * cospi(2.0 * d.u2);
+    const double v = mu[k] + sg[k] * z;
+    if (!bounded || (H.low <= v && v < H.high)) { x = v; ok = true; }
+  }
+  if (!ok) {
+    // truncated inverse CDF of the last component (rejection budget spent)
+    const double a = normal_cdf(H.low, mu[k], sg[k]);
+    const double b = normal_cdf(H.high, mu[k], sg[k]);
+    const double u = a + d.u3 * (b - a);
+    double v = mu[k] + sg[k] * 1.4142135623730951 * erfinv(2.0 * u - 1.0);
+    if (!(v >= H.low)) v = H.low;
+    if (!(v < H.high)) v = nextafter(H.high, -INFINITY);
+    x = v;
+  }
+  if (H.family == TPE_LGMM) x = exp(x);
+  if (H.flags & TPE_HAS_Q) x = rint(x / H.q) * H.q;
+  return x;
+}
+
+// ------------------------------------------------------------------------
+// scoring inner loops
+// ------------------------------------------------------------------------
+// log-sum-exp slice in log2 units: m = max_k t_k, s = sum_k 2^(t_k - m),
+// t_k = c_k - ((y - mu_k) a_k)^2.  Exponent arguments and the accumulator are
+// fp64; 2^(t-m) in [0,1] is one v_exp_f32 (rel. err ~1e-7 per term).
+__device__ __forceinline__ void lse_slice(const Coef *__restrict__ c, int k0, int k1,
+                                          double y, double &m_out, double &s_out) {
+  double m = -INFINITY;
+#pragma unroll 4
+  for (int k = k0; k < k1; ++k) {
+    const double z = (y - c[k].x) * c[k].y;
+    m = fmax(m, fma(-z, z, c[k].z));
+  }
+  double s = 0.0;
+  if (m != -INFINITY || !(fabs(y) < INFINITY)) {
+#pragma unroll 4
+    for (int k = k0; k < k1; ++k) {
+      const double z = (y - c[k].x) * c[k].y;
+      const double t = fma(-z, z, c[k].z);
+      s += (double)__builtin_amdgcn_exp2f((float)(t - m));
+    }
+  }
+  m_out = m;
+  s_out = s;
+}
+
+// linear-space sum of w_k (Phi_k(ub) - Phi_k(lb)), tpe.py:146-160 / 284-299.
+// Components with both bounds beyond 6.5 sigma on one side contribute an
+// exact 0 in float64 (erf saturates to +-1), so they are skipped.
+template <bool LOGN>
+__device__ __forceinline__ double erf_slice(const Coef *__restrict__ c, int k0,
+                                            int k1, double ub, double lb) {
+#pragma clang fp contract(off)
+  double prob = 0.0;
+  for (int k = k0; k < k1; ++k) {
+    const double zu = (ub - c[k].x) * c[k].y;
+    const double zl = (lb - c[k].x) * c[k].y;
+    const bool dead = (zu >= 6.5 && zl >= 6.5) || (zu <= -6.5 && zl <= -6.5);
+    if (!dead) {
+      const double wk = c[k].z;
+      double cu, cl;
+      if (LOGN) {
+        cu = .5 + .5 * erf(zu);
+        cl = .5 + .5 * erf(zl);
+      } else {
+        cu = 0.5 * (1.0 + erf(zu));
+        cl = 0.5 * (1.0 + erf(zl));
+      }
+      double inc = wk * cu;
+      inc -= wk * cl;
+      prob += inc;
+    }
+  }
+  return prob;
+}
+
+__device__ __forceinline__ bool better(double sa, int64_t ia, double sb, int64_t ib) {
+  if (ia < 0) return false;
+  if (ib < 0) return true;
+  const bool na = sa != sa, nb = sb != sb;
+  if (na || nb) return (na && nb) ? ia < ib : na;
+  if (sa != sb) return sa > sb;
+  return ia < ib;
+}
+
+__device__ __forceinline__ void wave_best(double &s, double &v, int64_t &i) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double os = __shfl_xor(s, o, 64);
+    const double ov = __shfl_xor(v, o, 64);
+    const int64_t oi = __shfl_xor(i, o, 64);
+    if (better(os, oi, s, i)) { s = os; v = ov; i = oi; }
+  }
+}
+
+__device__ __forceinline__ void slice_bounds(int K, int part, int parts, int &k0, int &k1) {
+  const int per = (K + parts - 1) / parts;
+  k0 = min(K, part * per);
+  k1 = min(K, k0 + per);
+}
+
+__device__ __forceinline__ bool hp_active(const tpe_hp &H, const Partial *res,
+                                          const int32_t *cp, const int32_t *cb) {
+  if (H.cond_count == 0) return true;
+  for (int c = 0; c < H.cond_count; ++c) {
+    const Partial &r = res[cp[H.cond_begin + c]];
+    if (r.active && r.index >= 0 && r.value == (double)cb[H.cond_begin + c]) return true;
+  }
+  return false;
+}
+
+// Candidate draws of one (level, kind) group: grid = (blocks, hps, suggestions).
+// Counter = (global candidate index, hp id, iteration), key = suggestion seed,
+// so the candidate set does not depend on how [0, n_cand) is sharded.
+__global__ __launch_bounds__(256) void k_draw(ScoreArgs A) {
+  const int slot = blockIdx.y, s = blockIdx.z;
+  const int hp = A.level_hps[slot];
+  const tpe_hp H = A.hps[hp];
+  if (!hp_active(H, A.results + (int64_t)s * A.n_hp, A.cond_parent, A.cond_branch)) return;
+  const int64_t sb = 2 * (int64_t)hp;
+  const MixInfo ib = A.info[sb];
+  const double *bw = A.mw + sb * A.kcap, *bmu = A.mmu + sb * A.kcap, *bsg = A.msig + sb * A.kcap;
+  const uint64_t seed = A.seeds[s];
+  double *out = const_cast<double *>(A.cand) + ((int64_t)s * A.n_slots + slot) * A.n_cand;
+  for (int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; li < A.n_cand;
+       li += (int64_t)gridDim.x * blockDim.x)
+    out[li] = draw_one(H, ib, bw, bmu, bsg, seed, (uint64_t)(A.cand_begin + li), (uint32_t)hp);
+}
+
+// Scoring kernel, one instantiation per lpdf kind so each keeps its own
+// register budget (the erf path must not cap the log-sum-exp path's
+// occupancy).  grid = (candidate-tile blocks, hps of the group, suggestions);
+// 4 waves per block; with ks > 1 the waves of a 64-candidate group split the
+// components and combine their partial sums through LDS.
+template <int KIND>
+__global__ __launch_bounds__(256) void k_score(ScoreArgs A, const Coef *__restrict__ coef,
+                                               const double *__restrict__ cand_all) {
+  constexpr bool LSE = KIND == KIND_LSE_G || KIND == KIND_LSE_L;
+  constexpr bool ERF = KIND == KIND_ERF_G || KIND == KIND_ERF_L;
+  constexpr bool CAT = KIND == KIND_CAT;
+  constexpr bool LOGN = KIND == KIND_LSE_L || KIND == KIND_ERF_L;
+  __shared__ double red[4][4][64];
+  __shared__ double bs[4], bv[4];
+  __shared__ int64_t bi[4];
+  const int slot = blockIdx.y, s = blockIdx.z;
+  const int hp = A.level_hps[slot];
+  const tpe_hp H = A.hps[hp];
+  Partial *pout = A.partial + ((int64_t)s * A.n_slots + slot) * gridDim.x + blockIdx.x;
+
+  const bool act = A.force_active || hp_active(H, A.results + (int64_t)s * A.n_hp,
+                                                  A.cond_parent, A.cond_branch);
+  if (!act) {
+    if (threadIdx.x == 0) *pout = Partial{NAN, NAN, -1, 0, 0};
+    return;
+  }
+  const int64_t sb = 2 * (int64_t)hp, sa = sb + 1;
+  const MixInfo ib = A.info[sb], ia = A.info[sa];
+  const Coef *__restrict__ cb = coef + sb * A.kcap;
+  const Coef *__restrict__ ca = coef + sa * A.kcap;
+  const double *__restrict__ cand = cand_all + ((int64_t)s * A.n_slots + slot) * A.n_cand;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int ks = A.ks, groups = 4 / ks;
+  const int grp = wave / ks, kp = wave % ks;
+  const int TC = 64 * groups;
+  int kb0 = 0, kb1 = 0, ka0 = 0, ka1 = 0;
+  slice_bounds(ib.K, kp, ks, kb0, kb1);
+  slice_bounds(ia.K, kp, ks, ka0, ka1);
+  // wave-uniform component ranges -> scalar (SGPR) component loads
+  kb0 = __builtin_amdgcn_readfirstlane(kb0);
+  kb1 = __builtin_amdgcn_readfirstlane(kb1);
+  ka0 = __builtin_amdgcn_readfirstlane(ka0);
+  ka1 = __builtin_amdgcn_readfirstlane(ka1);
+
+  double best_s = NAN, best_v = NAN;
+  int64_t best_i = -1;
+  for (int tile = blockIdx.x; tile < A.tiles; tile += gridDim.x) {
+    const int64_t li = (int64_t)tile * TC + grp * 64 + lane;
+    const bool valid = li < A.n_cand;
+    const double x = valid ? cand[li] : 0.0;
+    double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
+    if constexpr (LSE) {
+      const double y = LOGN ? log(x) : x;
+      lse_slice(cb, kb0, kb1, y, p0, p1);
+      lse_slice(ca, ka0, ka1, y, p2, p3);
+    } else if constexpr (ERF) {
+      const double hq = H.q / 2.0;
+      double ub, lb;
+      if constexpr (!LOGN) {
+        ub = (H.flags & TPE_HAS_HIGH) ? np_minimum(x + hq, H.high) : x + hq;
+        lb = (H.flags & TPE_HAS_LOW) ? np_maximum(x - hq, H.low) : x - hq;
+      } else {
+        const double u = (H.flags & TPE_HAS_HIGH) ? np_minimum(x + hq, exp(H.high)) : x + hq;
+        double l = (H.flags & TPE_HAS_LOW) ? np_maximum(x - hq, exp(H.low)) : x - hq;
+        l = np_maximum(0.0, l);
+        ub = u < 0.0 ? NAN : log(np_maximum(u, kEPS));
+        lb = log(np_maximum(l, kEPS));
+      }
+      p0 = erf_slice<LOGN>(cb, kb0, kb1, ub, lb);
+      p2 = erf_slice<LOGN>(ca, ka0, ka1, ub, lb);
+    }
+    if (!CAT && ks > 1) {
+      red[wave][0][lane] = p0; red[wave][1][lane] = p1;
+      red[wave][2][lane] = p2; red[wave][3][lane] = p3;
+      __syncthreads();
+    }
+    if (kp == 0 && valid) {
+      double lpb, lpa;
+      if constexpr (LSE) {
+        double mb = p0, smb = p1, ma = p2, sma = p3;
+        for (int j = 1; j < ks; ++j) {
+          const int wv = grp * ks + j;
+          const double m2 = red[wv][0][lane], s2 = red[wv][1][lane];
+          const double m4 = red[wv][2][lane], s4 = red[wv][3][lane];
+          if (m2 > mb) { smb = smb * exp2(mb - m2) + s2; mb = m2; }
+          else if (m2 != -INFINITY || s2 != s2) smb += s2 * exp2(m2 - mb);
+          if (m4 > ma) { sma = sma * exp2(ma - m4) + s4; ma = m4; }
+          else if (m4 != -INFINITY || s4 != s4) sma += s4 * exp2(m4 - ma);
+        }
+        const double LN2 = 0.6931471805599453;
+        lpb = (mb == -INFINITY) ? NAN : (mb + log2(smb)) * LN2;
+        lpa = (ma == -INFINITY) ? NAN : (ma + log2(sma)) * LN2;
+        if constexpr (LOGN) { const double lx = log(x); lpb -= lx; lpa -= lx; }
+      } else if constexpr (ERF) {
+        double pb = p0, pa = p2;
+        for (int j = 1; j < ks; ++j) {
+          pb += red[grp * ks + j][0][lane];
+          pa += red[grp * ks + j][2][lane];
+        }
+        lpb = log(pb) - ib.log_pacc;
+        lpa = log(pa) - ia.log_pacc;
+      } else {
+        const int64_t c = (int64_t)x;
+        const bool in = (x >= 0.0) && (c < ib.K) && ((double)c == x);
+        lpb = in ? cb[c].x : NAN;
+        lpa = in ? ca[c].x : NAN;
+      }
+      if (A.out_lb) A.out_lb[li] = lpb;
+      if (A.out_la) A.out_la[li] = lpa;
+      const int64_t gi = A.cand_begin + li;
+      const double sc = lpb - lpa;
+      if (better(sc, gi, best_s, best_i)) { best_s = sc; best_v = x; best_i = gi; }
+    }
+    if (!CAT && ks > 1) __syncthreads();
+  }
+  wave_best(best_s, best_v, best_i);
+  if (lane == 0) { bs[wave] = best_s; bv[wave] = best_v; bi[wave] = best_i; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; ++w)
+      if (better(bs[w], bi[w], best_s, best_i)) { best_s = bs[w]; best_v = bv[w]; best_i = bi[w]; }
+    *pout = Partial{best_s, best_v, best_i, 1, 0};
+  }
+}
+
+// grid reduce: one block per (slot, suggestion)
+__global__ __launch_bounds__(64) void k_reduce(const int32_t *__restrict__ level_hps,
+                                               int32_t n_slots, int32_t n_hp,
+                                               int32_t grid_x, int32_t accumulate,
+                                               const Partial *__restrict__ partial,
+                                               Partial *__restrict__ results) {
+  const int slot = blockIdx.x, s = blockIdx.y;
+  const Partial *p = partial + ((int64_t)s * n_slots + slot) * grid_x;
+  Partial *r = results + (int64_t)s * n_hp + level_hps[slot];
+  double bs_ = NAN, bv_ = NAN;
+  int64_t bi_ = -1;
+  const int active = grid_x > 0 ? p[0].active : 1;
+  for (int i = threadIdx.x; i < grid_x; i += 64)
+    if (better(p[i].score, p[i].index, bs_, bi_)) { bs_ = p[i].score; bv_ = p[i].value; bi_ = p[i].index; }
+  wave_best(bs_, bv_, bi_);
+  if (threadIdx.x == 0) {
+    if (accumulate && better(r->score, r->index, bs_, bi_)) return;
+    *r = Partial{bs_, bv_, active ? bi_ : -1, active, 0};
+  }
+}
+
+// cross-device merge of gathered [world][S][P] results
+__global__ __launch_bounds__(64) void k_merge(const int32_t *__restrict__ level_hps,
+                                              int32_t n_slots, int32_t n_suggest,
+                                              int32_t n_hp, int32_t world,
+                                              const Partial *__restrict__ g,
+                                              Partial *__restrict__ results) {
+  const int slot = blockIdx.x, s = blockIdx.y;
+  const int hp = level_hps[slot];
+  double bs_ = NAN, bv_ = NAN;
+  int64_t bi_ = -1;
+  int active = 0;
+  for (int r = threadIdx.x; r < world; r += 64) {
+    const Partial q = g[((int64_t)r * n_suggest + s) * n_hp + hp];
+    active |= q.active;
+    if (better(q.score, q.index, bs_, bi_)) { bs_ = q.score; bv_ = q.value; bi_ = q.index; }
+  }
+  wave_best(bs_, bv_, bi_);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) active |= __shfl_xor(active, o, 64);
+  if (threadIdx.x == 0)
+    results[(int64_t)s * n_hp + hp] = Partial{bs_, bv_, active ? bi_ : -1, active, 0};
+}
+
+__global__ __launch_bounds__(256) void k_sample(const tpe_hp *__restrict__ hpd,
+                                                const double *__restrict__ w,
+                                                const double *__restrict__ mu,
+                                                const double *__restrict__ sg,
+                                                const MixInfo *__restrict__ info,
+                                                uint64_t seed, uint32_t stream,
+                                                int64_t offset, int64_t n,
+                                                double *__restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const tpe_hp H = hpd[0];
+  const MixInfo I = info[0];
+  out[i] = draw_one(H, I, w, mu, sg, seed, (uint64_t)(offset + i), stream);
+}
+
+// ------------------------------------------------------------------------
+// launch wrappers
+// ------------------------------------------------------------------------
+hipError_t launch_split(const double *losses, int64_t n, int32_t n_below, uint8_t *below,
+                        hipStream_t st) {
+  k_split<<<1, 1024, 0, st>>>(losses, n, n_below, below);
+  return hipGetLastError();
+}
+
+hipError_t launch_fit(const tpe_hp *hps, int32_t n_hp, const double *vals,
+                      const uint8_t *active, const uint8_t *below, int64_t n,
+                      double prior_weight, int32_t lf, const double *pprior, double *mw,
+                      double *mmu, double *msig, MixInfo *info, int64_t kcap,
+                      double *scratch, hipStream_t st) {
+  if (n_hp <= 0) return hipSuccess;
+  const size_t lds = (size_t)(n < 12288 ? n : 12288) * 8;
+  k_fit<<<dim3(n_hp, 2), 1024, lds, st>>>(hps, vals, active, below, n, prior_weight, lf,
+                                          pprior, mw, mmu, msig, info, kcap, scratch);
+  return hipGetLastError();
+}
+
+hipError_t launch_prep(const tpe_hp *hps, int32_t n_hp, const double *mw, const double *mmu,
+                       const double *msig, MixInfo *info, Coef *coef, int64_t kcap,
+                       double *scratch, hipStream_t st) {
+  if (n_hp <= 0) return hipSuccess;
+  k_prep<<<dim3(n_hp, 2), 256, 0, st>>>(hps, mw, mmu, msig, info, coef, kcap, scratch);
+  return hipGetLastError();
+}
+
+hipError_t launch_score(const ScoreArgs &a, int32_t kind, int32_t grid_x, hipStream_t st) {
+  if (a.n_slots <= 0) return hipSuccess;
+  if (a.n_suggest <= 0) return hipSuccess;
+  const dim3 g(grid_x, a.n_slots, a.n_suggest);
+  switch (kind) {
+    case KIND_LSE_G: k_score<KIND_LSE_G><<<g, 256, 0, st>>>(a, a.coef, a.cand); break;
+    case KIND_LSE_L: k_score<KIND_LSE_L><<<g, 256, 0, st>>>(a, a.coef, a.cand); break;
+    case KIND_ERF_G: k_score<KIND_ERF_G><<<g, 256, 0, st>>>(a, a.coef, a.cand); break;
+    case KIND_ERF_L: k_score<KIND_ERF_L><<<g, 256, 0, st>>>(a, a.coef, a.cand); break;
+    default: k_score<KIND_CAT><<<g, 256, 0, st>>>(a, a.coef, a.cand); break;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_draw(const ScoreArgs &a, hipStream_t st) {
+  if (a.n_slots <= 0 || a.n_suggest <= 0 || a.n_cand <= 0) return hipSuccess;
+  const int64_t want = (a.n_cand + 255) / 256;
+  const int64_t cap = std::max<int64_t>(1, 8192 / ((int64_t)a.n_slots * a.n_suggest));
+  const unsigned gx = (unsigned)std::max<int64_t>(1, std::min(want, cap));
+  k_draw<<<dim3(gx, a.n_slots, a.n_suggest), 256, 0, st>>>(a);
+  return hipGetLastError();
+}
+
+hipError_t launch_reduce(const int32_t *level_hps, int32_t n_slots, int32_t n_suggest,
+                         int32_t n_hp, int32_t grid_x, int32_t accumulate,
+                         const Partial *partial, Partial *results, hipStream_t st) {
+  if (n_slots <= 0 || n_suggest <= 0) return hipSuccess;
+  k_reduce<<<dim3(n_slots, n_suggest), 64, 0, st>>>(level_hps, n_slots, n_hp, grid_x, accumulate,
+                                                    partial, results);
+  return hipGetLastError();
+}
+
+hipError_t launch_merge(const int32_t *level_hps, int32_t n_slots, int32_t n_suggest,
+                        int32_t n_hp, int32_t world, const Partial *gathered,
+                        Partial *results, hipStream_t st) {
+  if (n_slots <= 0 || n_suggest <= 0) return hipSuccess;
+  k_merge<<<dim3(n_slots, n_suggest), 64, 0, st>>>(level_hps, n_slots, n_suggest, n_hp, world,
+                                                   gathered, results);
+  return hipGetLastError();
+}
+
+hipError_t launch_sample(const tpe_hp *hp_dev, const double *mw, const double *mmu,
+                         const double *msig, const MixInfo *info, uint64_t seed,
+                         uint64_t stream, int64_t offset, int64_t n, double *out,
+                         hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int64_t blocks = (n + 255) / 256;
+  k_sample<<<(unsigned)blocks, 256, 0, st>>>(hp_dev, mw, mmu, msig, info, seed, (uint32_t)stream,
+                                             offset, n, out);
+  return hipGetLastError();
+}
+
+}  // namespace tpe

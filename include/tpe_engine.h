@@ -1,0 +1,196 @@
+/*
+ * tpe_engine.h -- C ABI of the MI355X (gfx950) TPE suggestion engine.
+ *
+ * Drop-in boundary.  The reference (pminervini/hyperopt, pure Python/numpy)
+ * has no FFI of its own; its hot path is a set of pyll `scope` operators
+ * evaluated per hyperparameter inside `tpe.suggest`.  Each entry point below
+ * replaces one of those operators (operator level, host buffers, synchronous)
+ * or the whole evaluation of the posterior graph (plan level, device
+ * resident).  The Python binding is hyperopt_amd/_engine.py (ctypes); see
+ * INTEGRATION.md for the binding a reference maintainer would add.
+ *
+ * Conventions: all functions return TPE_OK (0) or a negative TPE_E_* code;
+ * tpe_last_error() gives the message.  No exception or abort crosses the ABI.
+ * Inputs are never mutated.  One handle must be used by one thread at a
+ * time; distinct handles are independent (no global mutable state).
+ */
+#ifndef TPE_ENGINE_H
+#define TPE_ENGINE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TPE_ENGINE_ABI_VERSION 1
+
+/* ---- status codes ---------------------------------------------------- */
+#define TPE_OK 0
+#define TPE_E_INVALID (-1)   /* bad argument / shape  -> TypeError/ValueError     */
+#define TPE_E_BOUNDS (-2)    /* low >= high           (tpe.py:80-81, 237-238)     */
+#define TPE_E_NEGATIVE (-3)  /* negative lognormal_cdf argument (tpe.py:181-182) */
+#define TPE_E_NOMEM (-4)     /* device allocation failed                         */
+#define TPE_E_HIP (-5)       /* HIP runtime error                                */
+#define TPE_E_NODEVICE (-6)  /* no gfx950 device                                 */
+#define TPE_E_INDEX (-7)     /* categorical sample out of range (IndexError)     */
+
+/* ---- posterior families ---------------------------------------------- */
+#define TPE_GMM 0  /* GMM1 / GMM1_lpdf          hyperopt/tpe.py:62-166  */
+#define TPE_LGMM 1 /* LGMM1 / LGMM1_lpdf        hyperopt/tpe.py:216-301 */
+#define TPE_CAT 2  /* categorical / _lpdf       hyperopt/tpe.py:50-57, 573-607 */
+
+/* ---- flags (which optional lpdf / sampler arguments are not None) ----- */
+#define TPE_HAS_LOW 1u
+#define TPE_HAS_HIGH 2u
+#define TPE_HAS_Q 4u
+#define TPE_PCHOICE 8u /* categorical with a prior p (hp.pchoice) */
+
+/* ---- observation transform applied before the Parzen fit --------------
+ * hyperopt/tpe.py:485-568 (ap_*_sampler).                                  */
+#define TPE_OBS_IDENT 0          /* uniform, quniform, normal, qnormal        */
+#define TPE_OBS_LOG 1            /* loguniform, lognormal: log(obs)           */
+#define TPE_OBS_LOG_CLIP_EXPLOW 2/* qloguniform: log(max(obs, max(EPS, e^low))) */
+#define TPE_OBS_LOG_CLIP_EPS 3   /* qlognormal: log(max(obs, EPS))            */
+
+typedef struct tpe_engine *tpe_handle_t;
+typedef struct tpe_plan *tpe_plan_t;
+
+/* One hyperparameter of a compiled search space (descriptor
+ * table).  For TPE_LGMM, low/high are the log-space bounds exactly as the
+ * reference passes them to LGMM1/LGMM1_lpdf. */
+typedef struct {
+  int32_t family;        /* TPE_GMM / TPE_LGMM / TPE_CAT                  */
+  uint32_t flags;        /* TPE_HAS_* / TPE_PCHOICE                       */
+  int32_t obs_transform; /* TPE_OBS_*                                     */
+  int32_t upper;         /* categorical: number of categories             */
+  double prior_mu;       /* Parzen prior (continuous families)            */
+  double prior_sigma;
+  double low, high, q;   /* sampler / lpdf arguments (valid per flags)    */
+  int32_t cond_begin;    /* activity: OR over [cond_begin, +cond_count) of */
+  int32_t cond_count;    /*   (parent active && parent value == branch)    */
+  int64_t pprior_begin;  /* TPE_PCHOICE: upper probabilities in pprior[]   */
+} tpe_hp;
+
+typedef struct {
+  int32_t n_hp;
+  const tpe_hp *hp;
+  int32_t n_cond;
+  const int32_t *cond_parent; /* hp index of the controlling choice   */
+  const int32_t *cond_branch; /* option index that activates the hp   */
+  int64_t n_pprior;
+  const double *pprior;
+} tpe_space;
+
+/* Per (suggestion, hp) outcome of broadcast_best (tpe.py:749-759). */
+typedef struct {
+  double score;  /* below_llik - above_llik of the winner (NaN allowed)   */
+  double value;  /* the winning candidate                                 */
+  int64_t index; /* its global candidate index (-1: hp inactive)          */
+  int32_t active;/* 1 if the hp is active in this suggestion              */
+  int32_t pad;
+} tpe_result;
+
+/* ---- engine ------------------------------------------------------------ */
+const char *tpe_version(void);
+int tpe_device_count(int32_t *n);
+int tpe_create(int32_t device, tpe_handle_t *out);
+int tpe_destroy(tpe_handle_t h);
+const char *tpe_last_error(tpe_handle_t h);
+int tpe_synchronize(tpe_handle_t h);
+
+/* ---- operator level: host buffers, synchronous -------------------------
+ * Each mirrors one pyll scope operator of the reference.                   */
+
+/* ap_filter_trials loss ranking (tpe.py:613-641): marks the n_below lowest
+ * losses (ties: lowest position first) with 1 in below_mask[n].           */
+int tpe_split(tpe_handle_t h, const double *losses, int64_t n, double gamma,
+              int32_t gamma_cap, uint8_t *below_mask);
+
+/* adaptive_parzen_normal (tpe.py:398-475): K = n + 1 outputs.             */
+int tpe_parzen_fit(tpe_handle_t h, const double *obs, int64_t n,
+                   double prior_weight, double prior_mu, double prior_sigma,
+                   int32_t lf, double *w, double *mu, double *sigma);
+
+/* categorical posterior (tpe.py:573-607): p[upper].  pprior may be NULL.  */
+int tpe_categorical_posterior(tpe_handle_t h, const int64_t *obs, int64_t n,
+                              int32_t upper, double prior_weight,
+                              const double *pprior, int32_t lf, double *p);
+
+/* GMM1_lpdf / LGMM1_lpdf (tpe.py:104-166, 259-301) of one mixture.  For
+ * TPE_CAT, w holds p (k = upper) and mu/sigma are ignored.                */
+int tpe_lpdf(tpe_handle_t h, int32_t family, const double *x, int64_t n,
+             const double *w, const double *mu, const double *sigma, int64_t k,
+             double low, double high, double q, uint32_t flags, double *out);
+
+/* Fused below/above lpdf + broadcast_best argmax (tpe.py:684-698, 749-759).
+ * llik_b / llik_a may be NULL (argmax only).                               */
+int tpe_score(tpe_handle_t h, int32_t family, const double *x, int64_t n,
+              const double *wb, const double *mb, const double *sb, int64_t kb,
+              const double *wa, const double *ma, const double *sa, int64_t ka,
+              double low, double high, double q, uint32_t flags,
+              double *llik_b, double *llik_a, int64_t *best_index,
+              double *best_score);
+
+/* GMM1 / LGMM1 / categorical candidate draws (tpe.py:62-93, 216-250,
+ * pyll/stochastic.py:104-142) with counter-based Philox4x32-10: draw i uses
+ * counter (offset + i, stream), key seed, so any sharding of [0, n) yields
+ * the same values.                                                        */
+int tpe_sample(tpe_handle_t h, int32_t family, const double *w,
+               const double *mu, const double *sigma, int64_t k, double low,
+               double high, double q, uint32_t flags, uint64_t seed,
+               uint64_t stream, int64_t offset, int64_t n, double *out);
+
+/* ---- plan level: whole tpe.suggest posterior evaluation on device -------
+ * A plan holds one compiled space and a device-resident trial history.     */
+int tpe_plan_create(tpe_handle_t h, const tpe_space *space, int64_t max_trials,
+                    tpe_plan_t *out);
+int tpe_plan_destroy(tpe_plan_t p);
+int tpe_plan_num_levels(tpe_plan_t p, int32_t *n_levels);
+
+/* History in tid order (tpe.py:820-848): losses[n] (+inf for unfinished),
+ * vals[n_hp][n], active[n_hp][n].  on_device != 0: pointers are device
+ * memory (e.g. torch tensors); stream: hipStream_t or NULL.                */
+int tpe_plan_set_history(tpe_plan_t p, const double *losses,
+                         const double *vals, const uint8_t *active, int64_t n,
+                         int32_t on_device, void *stream);
+
+/* split + Parzen fit of every hp, both sides (tpe.py:613-641, 398-607).    */
+int tpe_plan_fit(tpe_plan_t p, double gamma, int32_t gamma_cap,
+                 double prior_weight, int32_t lf, void *stream);
+
+/* Below-side mixture of one hp after tpe_plan_fit (host copy; k = K).     */
+int tpe_plan_get_mixture(tpe_plan_t p, int32_t hp, int32_t side, double *w,
+                         double *mu, double *sigma, int64_t cap, int64_t *k);
+
+/* Sample + score + argmax for n_suggest suggestions (seeds[s]) on the
+ * candidate range [cand_begin, cand_begin + n_cand) of each suggestion, for
+ * the hps of one level (level < 0: all levels, single device).  Results for
+ * [n_suggest][n_hp] are kept in the plan; out (host or device, may be NULL)
+ * receives a copy.                                                         */
+int tpe_plan_suggest(tpe_plan_t p, const uint64_t *seeds, int64_t n_suggest,
+                     int64_t n_cand, int64_t cand_begin, int32_t level,
+                     tpe_result *out, int32_t out_on_device, void *stream);
+
+/* Multi-device: combine world copies of one level's results ([world][S][P],
+ * device memory, e.g. an RCCL all-gather) with numpy argmax semantics and
+ * make them the plan's state.                                              */
+int tpe_plan_merge(tpe_plan_t p, const tpe_result *gathered, int32_t world,
+                   int32_t level, tpe_result *out, int32_t out_on_device,
+                   void *stream);
+
+/* Score given candidates of one hp with the plan's fitted mixtures
+ * (parity path for reference-sampled candidates).                          */
+int tpe_plan_score_candidates(tpe_plan_t p, int32_t hp, const double *x,
+                              int64_t n, double *llik_b, double *llik_a,
+                              int64_t *best_index, double *best_score);
+
+/* Device time (ms) of the last tpe_plan_suggest's scoring launches, from
+ * HIP events on the plan's stream; and the (candidate, component) pairs
+ * they evaluated.                                                          */
+int tpe_plan_last_stats(tpe_plan_t p, double *score_ms, double *pairs);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TPE_ENGINE_H */

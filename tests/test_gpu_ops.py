@@ -1,0 +1,191 @@
+"""GPU parity of the operator-level C ABI against the reference's golden
+vectors and the CPU oracle.  Every call goes through libtpe_engine.so."""
+import numpy as np
+import pytest
+
+from golden_io import load, load_json, unpack, ncases, opt
+from gpu_util import assert_close, argmax_equiv, close
+from oracle import tpe_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def eng():
+    from hyperopt_amd._engine import Engine
+    return Engine(0)
+
+
+def test_split_matches_oracle(eng):
+    d = load('split.npz')
+    for i in range(len(d['gamma'])):
+        losses = unpack(d, 'losses', i)
+        tids = unpack(d, 'tids', i)
+        mask = eng.split(losses, d['gamma'][i])
+        good, _ = O.below_tids(tids, losses, d['gamma'][i], kind='stable')
+        assert set(tids[mask].tolist()) == good
+        if len(np.unique(losses)) == len(losses):   # no ties: == reference
+            ot, ov = unpack(d, 'o_tids', i), unpack(d, 'o_vals', i)
+            keep = set(tids[mask].tolist())
+            below = np.array([v for t, v in zip(ot, ov) if t in keep])
+            np.testing.assert_array_equal(below, unpack(d, 'below', i))
+
+
+def test_parzen_bit_exact(eng):
+    d = load('parzen.npz')
+    for i in range(ncases(d, 'obs')):
+        obs = unpack(d, 'obs', i)
+        pw, pm, ps = d['prior'][i]
+        w, mu, sg = eng.parzen_fit(obs, pw, pm, ps)
+        if len(np.unique(obs)) == len(obs):
+            ref = (unpack(d, 'w', i), unpack(d, 'mu', i), unpack(d, 'sigma', i))
+        else:   # tied observations: the engine's sort is stable
+            ref = O.parzen_fit(obs, pw, pm, ps, kind='stable')
+        np.testing.assert_array_equal(mu, ref[1], err_msg='case %d mu' % i)
+        np.testing.assert_array_equal(sg, ref[2], err_msg='case %d sigma' % i)
+        np.testing.assert_array_equal(w, ref[0], err_msg='case %d w' % i)
+
+
+def test_categorical_posterior(eng):
+    d = load('categorical.npz')
+    for i in range(len(d['upper'])):
+        obs = unpack(d, 'obs', i)
+        pp = unpack(d, 'pprior', i)
+        pp = None if np.isnan(pp).all() else pp
+        p = eng.categorical_posterior(obs, int(d['upper'][i]), d['pw'][i], pp)
+        np.testing.assert_array_equal(p, unpack(d, 'p', i))
+
+
+def test_score_matches_reference(eng):
+    from hyperopt_amd._engine import GMM, LGMM
+    d = load('lpdf.npz')
+    names = load_json('lpdf_names.json')
+    for i, nm in enumerate(names):
+        lg, low, high, q = d['meta'][i]
+        low, high, q = opt(low), opt(high), opt(q)
+        mb = unpack(d, 'mix_b', i).reshape(3, -1)
+        ma = unpack(d, 'mix_a', i).reshape(3, -1)
+        x = unpack(d, 'cand', i)
+        lb, la, bi, bs = eng.score(LGMM if lg else GMM, x, mb, ma, low, high, q)
+        rb, ra = unpack(d, 'llik_b', i), unpack(d, 'llik_a', i)
+        assert_close(lb, rb, msg=nm + ' below')
+        assert_close(la, ra, msg=nm + ' above')
+        with np.errstate(all='ignore'):
+            assert argmax_equiv(rb - ra, bi), (nm, bi, d['best'][i])
+
+
+def test_lpdf_closed_form(eng):
+    """hyperopt/tests/test_tpe.py:105-190 closed-form GMM1_lpdf values."""
+    from hyperopt_amd._engine import GMM
+    w, mu, sg = [0.25, 0.25, .5], [0.0, 1.0, 2.0], [1.0, 2.0, 5.0]
+    a1 = (.25 / np.sqrt(2 * np.pi * 1.0 ** 2) * np.exp(-.5 * 1.0 ** 2)
+          + .25 / np.sqrt(2 * np.pi * 2.0 ** 2)
+          + .5 / np.sqrt(2 * np.pi * 5.0 ** 2) * np.exp(-.5 * (1.0 / 5.0) ** 2))
+    a0 = (.25 / np.sqrt(2 * np.pi * 1.0 ** 2)
+          + .25 / np.sqrt(2 * np.pi * 2.0 ** 2) * np.exp(-.5 * (1.0 / 2.0) ** 2)
+          + .5 / np.sqrt(2 * np.pi * 5.0 ** 2) * np.exp(-.5 * (2.0 / 5.0) ** 2))
+    v = eng.lpdf(GMM, [[1.0, 0.0, 0.0], [0, 0, 1], [0, 0, 1000]], w, mu, sg)
+    assert v.shape == (3, 3)
+    assert np.allclose(v[0, 0], np.log(a1)) and np.allclose(v[1, 2], np.log(a1))
+    for ij in ((0, 1), (0, 2), (1, 0), (1, 1), (2, 0), (2, 1)):
+        assert np.allclose(v[ij], np.log(a0))
+    assert np.isfinite(v[2, 2])
+    one = eng.lpdf(GMM, [1.0], [1.], [1.0], [2.0])
+    assert np.allclose(one, np.log(1.0 / np.sqrt(2 * np.pi * 2.0 ** 2)))
+
+
+def test_score_errors_map_to_reference_exceptions(eng):
+    from hyperopt_amd._engine import GMM, CAT
+    mix = ([1.0], [0.0], [1.0])
+    with pytest.raises(ValueError):
+        eng.score(GMM, [0.0], mix, mix, low=1.0, high=0.0)
+    with pytest.raises(IndexError):
+        eng.score(CAT, [3.0], [0.5, 0.5], [0.5, 0.5])
+    lb, la, bi, bs = eng.score(GMM, [], mix, mix)
+    assert bi == -1
+
+
+# ---- statistical sampler parity (hyperopt/tests/test_tpe.py:193-514) -----
+def _hist_check(samples, lpdf_fn, per_bin=500):
+    samples = np.sort(samples)
+    edges = samples[::per_bin]
+    pdf = np.exp(lpdf_fn(edges[:-1]))
+    dx = edges[1:] - edges[:-1]
+    y = 1 / dx / len(dx)
+    err = (pdf - y) ** 2
+    assert np.max(err) < .1 and np.mean(err) < .01 and np.median(err) < .01, err
+
+
+@pytest.mark.parametrize('bounds', [(None, None), (2.5, 3.5)])
+def test_gmm_sampler_matches_lpdf(eng, bounds):
+    from hyperopt_amd._engine import GMM
+    w, mu, sg = [.1, .3, .4, .2], [1.0, 2.0, 3.0, 4.0], [.1, .4, .8, 2.0]
+    low, high = bounds
+    x = eng.sample(GMM, w, mu, sg, low=low, high=high, seed=234, n=10001)
+    if low is not None:
+        assert np.all((x >= low) & (x < high))
+    _hist_check(x, lambda e: O.gmm_lpdf(e, w, mu, sg, low=low, high=high))
+
+
+@pytest.mark.parametrize('q,bounds', [(1, (None, None)), (2, (None, None)), (0.5, (None, None)),
+                                      (1, (2, 4)), (2, (2, 4)), (1, (1, 4.1))])
+def test_qgmm_sampler_matches_lpdf(eng, q, bounds):
+    from hyperopt_amd._engine import GMM
+    w, mu, sg = [.1, .3, .4, .2], [1.0, 2.0, 3.0, 4.0], [.1, .4, .8, 2.0]
+    low, high = bounds
+    s = eng.sample(GMM, w, mu, sg, low=low, high=high, q=q, seed=234, n=1001) / q
+    assert np.all(s == s.astype(int))
+    lo = int(s.min())
+    counts = np.bincount(s.astype(int) - lo)
+    xc = np.arange(lo, int(s.max()) + 1) * q
+    prob = np.exp(O.gmm_lpdf(xc, w, mu, sg, low=low, high=high, q=q))
+    err = (prob - counts / 1001.0) ** 2
+    assert np.max(err) < .1 and np.mean(err) < .01 and np.median(err) < .01
+
+
+def _mix_cdf(x, w, mu, sg, low, high, log_space):
+    from scipy.stats import norm
+    t = np.log(x) if log_space else x
+    w, mu, sg = (np.asarray(a, dtype=float) for a in (w, mu, sg))
+    F = (w * norm.cdf((t[:, None] - mu) / sg)).sum(1)
+    if low is None:
+        return F / w.sum()
+    lo = (w * norm.cdf((low - mu) / sg)).sum()
+    hi = (w * norm.cdf((high - mu) / sg)).sum()
+    return (F - lo) / (hi - lo)
+
+
+@pytest.mark.parametrize('log_space', [False, True])
+@pytest.mark.parametrize('bounds', [(None, None), (2, 4), (-1.5, 0.5)])
+def test_sampler_ks(eng, log_space, bounds):
+    """Kolmogorov-Smirnov test of GMM1/LGMM1 draws against the mixture CDF.
+    (The reference's LGMM1 histogram test, test_tpe.py:415-458, passes only
+    for its RandomState(234) stream; with the reference's own sampler it
+    fails for 35% of seeds, so the Philox stream is checked with KS.)"""
+    from scipy.stats import kstest
+    from hyperopt_amd._engine import GMM, LGMM
+    w, mu, sg = [.1, .3, .4, .2], [-2.0, 1.0, 0.0, 3.0], [.1, .4, .8, 2.0]
+    low, high = bounds
+    x = eng.sample(LGMM if log_space else GMM, w, mu, sg, low=low, high=high, seed=7, n=20000)
+    if low is not None:
+        t = np.log(x) if log_space else x
+        assert np.all((t >= low) & (t < high))
+    res = kstest(x, lambda v: _mix_cdf(np.atleast_1d(v), w, mu, sg, low, high, log_space))
+    assert res.pvalue > 1e-3, res
+
+
+def test_sampler_counter_based_sharding(eng):
+    from hyperopt_amd._engine import GMM
+    w, mu, sg = [.5, .5], [0.0, 1.0], [1.0, 0.3]
+    full = eng.sample(GMM, w, mu, sg, low=-1, high=2, seed=99, stream=3, offset=0, n=1000)
+    a = eng.sample(GMM, w, mu, sg, low=-1, high=2, seed=99, stream=3, offset=0, n=377)
+    b = eng.sample(GMM, w, mu, sg, low=-1, high=2, seed=99, stream=3, offset=377, n=623)
+    np.testing.assert_array_equal(full, np.concatenate([a, b]))
+
+
+def test_categorical_sampler(eng):
+    from hyperopt_amd._engine import CAT
+    p = np.array([.1, .2, .3, .4])
+    x = eng.sample(CAT, p, seed=5, n=200000)
+    freq = np.bincount(x.astype(int), minlength=4) / x.size
+    assert np.allclose(freq, p, atol=5e-3)
