@@ -1,0 +1,238 @@
+#!/usr/bin/env python3
+"""bench.py -- TPE candidate-scoring throughput of the MI355X engine.
+
+Metric (BASELINE.json): "EI candidates scored/sec (x components)" = (candidate,
+mixture-component) lpdf pairs per second, plus tpe.suggest latency.
+
+One *step* = one whole device-side ``tpe.suggest`` posterior pass over the
+config's synthetic history, resident in HBM: good/bad split, both Parzen fits
+of every hyperparameter, Philox candidate draws, below/above lpdf of every
+candidate against every component, EI argmax.  Default workload: BASELINE
+configs[1] = config 2 (20-D mixed space, 1000-trial history, 4096 candidates).
+
+Multi-GPU (torch.distributed.run, one rank per GPU): weak scaling, each rank
+serves its own asynchronous suggestion (distinct seed) on the shared history,
+no collective inside the timed region (batched suggestions shard with no data
+exchange; the in-suggest candidate sharding + RCCL max-loc path lives in
+hyperopt_amd/parallel.py and is exercised by --mode shard).
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, 'tests'))
+
+
+def build_workload(cfg):
+    """(domain, losses, vals, active, n_cand, description)."""
+    import spaces
+    from hyperopt_amd import hp, rand, Trials
+    from hyperopt_amd.base import Domain
+    from hyperopt_amd.tpe import build_history
+    if cfg == 'cfg2':
+        dom = Domain(lambda x: 0.0, spaces.cfg2_space(hp))
+        n_hist, n_cand = 1000, 4096
+    elif cfg == 'cfg3':
+        dom = Domain(lambda x: 0.0, spaces.cfg3_space(hp))
+        n_hist, n_cand = 10000, 100000
+    elif cfg == 'cfg4':
+        dom = Domain(lambda x: 0.0, spaces.cfg4_space(hp))
+        n_hist, n_cand = 10000, 10_000_000
+    else:
+        raise ValueError(cfg)
+    losses = np.random.RandomState(2).rand(n_hist)
+    if cfg == 'cfg4':   # obs RandomState(1).uniform(-5,5,(1e4,100))
+        vals = np.random.RandomState(1).uniform(-5, 5, (n_hist, 100)).T.copy()
+        idx = np.array([int(l[1:]) for l in dom.space.labels])   # labels sort as strings
+        vals = np.ascontiguousarray(vals[idx])
+        active = np.ones_like(vals, dtype=np.uint8)
+    else:
+        docs = rand.suggest(list(range(n_hist)), dom, Trials(), 1)
+        for d, l in zip(docs, losses):
+            d['state'] = 2
+            d['result'] = {'status': 'ok', 'loss': float(l)}
+        from hyperopt_amd import trials_from_docs
+        t = trials_from_docs(docs, validate=False)
+        _, losses, vals, active = build_history(dom, t, dom.space.labels)
+    return dom, losses, vals, active, n_cand
+
+
+def cpu_baseline(dom, losses, vals, active, n_cand, budget_s):
+    """The oracle (numpy restatement, pinned to the reference) timed on one
+    host core over whole config-2 suggests; pairs as the GPU counts them."""
+    os.environ.setdefault('OPENBLAS_NUM_THREADS', '1')
+    from oracle import tpe_oracle as O
+    import spaces
+    cs = dom.space
+    hps = {h.label: dict(dist=h.dist, args=h.args,
+                         conds=tuple(p for p in (h.paths[0] if h.paths else ()))) for h in cs.hps}
+    tids = np.arange(losses.size)
+    obs = {h.label: (tids[active[h.index] == 1], vals[h.index][active[h.index] == 1])
+           for h in cs.hps}
+    runs, t_total, pairs = 0, 0.0, 0.0
+    with np.errstate(all='ignore'):
+        while t_total < budget_s or runs == 0:
+            t0 = time.perf_counter()
+            chosen, det = O.suggest_reference_stream(hps, tids, losses, obs, 7 + runs,
+                                                     n_ei=n_cand)
+            t_total += time.perf_counter() - t0
+            runs += 1
+            for lab, dd in det.items():
+                if cs.by_label[lab].is_categorical or len(dd['cand']) == 0:
+                    continue
+                pairs += len(dd['cand']) * (len(dd['below'][0]) + len(dd['above'][0]))
+    return dict(value=pairs / t_total, unit='pairs/s', cores=1, kind='port',
+                sample='%d whole config-2 suggests (%d candidates each) through the oracle '
+                       '(numpy/scipy float64 restatement of tpe.py, bit-equal to reference '
+                       'fixtures), single thread, %.1f s' % (runs, n_cand, t_total),
+                suggest_s=t_total / runs)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=50)
+    ap.add_argument('--warmup', type=int, default=10)
+    ap.add_argument('--config', default='cfg2', choices=['cfg2', 'cfg3', 'cfg4'])
+    ap.add_argument('--cpu-seconds', type=float, default=12.0)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--traffic-json', default=os.path.join(ROOT, 'profiles', 'traffic.json'))
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    import torch
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+
+    from hyperopt_amd import _engine as E
+    eng = E.Engine(local)
+    dom, losses, vals, active, n_cand = build_workload(args.config)
+    hps, conds, pprior = dom.space.engine_tables()
+    plan = E.Plan(eng, hps, conds, pprior, max_trials=losses.size)
+    # history resident in HBM before the timed region
+    d_losses = torch.from_numpy(np.ascontiguousarray(losses)).cuda()
+    d_vals = torch.from_numpy(np.ascontiguousarray(vals)).cuda()
+    d_act = torch.from_numpy(np.ascontiguousarray(active)).cuda()
+    torch.cuda.synchronize()
+    plan.set_history_device(d_losses.data_ptr(), d_vals.data_ptr(), d_act.data_ptr(),
+                            losses.size)
+    out = torch.empty(plan.n_hp * E.RESULT_DTYPE.itemsize, dtype=torch.uint8, device='cuda')
+
+    def step(i):
+        plan.fit(gamma=0.25, prior_weight=1.0, lf=25)
+        plan.suggest([1_000_003 * rank + 17 * i + 7], n_cand, out=out.data_ptr())
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    plan.profile(args.steps)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device='cuda')
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    _, pairs_step = plan.last_stats()
+    kernels = {}
+    for kind, name in enumerate(E.KIND_NAMES):
+        ms, n, pairs = plan.profile_read(kind)
+        if n:
+            kernels[name] = dict(avg_ms=ms, launches_per_step=n / args.steps,
+                                 pairs_per_launch=pairs,
+                                 pairs_per_s=(pairs / (ms * 1e-3)) if ms > 0 else None)
+    value = world * pairs_step * args.steps / elapsed
+
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+    # ---- roofline of the dominant scoring kernel ------------------------------
+    dom_name = max(kernels, key=lambda k: kernels[k]['avg_ms'] * kernels[k]['launches_per_step'])
+    kd = kernels[dom_name]
+    pps = kd['pairs_per_s'] or 0.0
+    if dom_name.startswith('erf'):
+        peak = eng.microbench(2)            # OCML fp64 erf / s, register-only
+        roof = dict(bound='transcendental', unit='Gerf/s', achieved=2 * pps / 1e9,
+                    peak=peak / 1e9, note='2 fp64 erf per pair (tpe.py:146-160); peak = '
+                    'measured register-only OCML erf rate')
+    else:
+        peak = eng.microbench(1)            # fp64 FMA flop/s
+        roof = dict(bound='valu', unit='TFLOP/s', achieved=6 * pps / 1e12, peak=peak / 1e12,
+                    note='6 fp64 flops + 1 exp per pair (SURVEY 8d); peak = measured '
+                    'register-only fp64 FMA rate')
+    roof['frac'] = roof['achieved'] / roof['peak'] if roof['peak'] else None
+    roof['kernel'] = 'k_score<%s>' % dom_name
+    roof['avg_launch_ms'] = kd['avg_ms']
+    roof['pairs_per_launch'] = kd['pairs_per_launch']
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            with open(args.traffic_json) as f:
+                traffic = json.load(f).get(args.config, {}).get(dom_name)
+        except Exception:
+            traffic = None
+    roof['traffic'] = traffic
+    roof['exp_peak_per_s'] = eng.microbench(0)
+
+    cpu = None
+    if not args.no_cpu_baseline and world == 1:
+        cpu = cpu_baseline(dom, losses, vals, active, n_cand if args.config == 'cfg2' else 4096,
+                           args.cpu_seconds)
+
+    line = {
+        'metric': 'EI candidates scored/sec (x components)',
+        'value': value,
+        'unit': 'pairs/s',
+        'n_gpus': world,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': 1e3 * elapsed / args.steps,
+        'higher_is_better': True,
+        'scaling': 'weak',
+        'vs_baseline': None,
+        'dtype': 'f64',
+        'data': 'synthetic (rand.suggest startup history, RandomState(2) losses)',
+        'config': {
+            'workload': {'cfg2': 'config 2: 20-D mixed space, 1000-trial history, 4096 '
+                                 'candidates/suggest', 'cfg3': 'config 3: 50-hp conditional, '
+                                 '1e4 history, 1e5 candidates', 'cfg4': 'config 4: 100-D, 1e4 '
+                                 'history, 1e7 candidates'}[args.config],
+            'pairs_per_suggest': pairs_step,
+            'suggest_latency_ms': 1e3 * elapsed / args.steps,
+            'parallelism': 'replicas' if world > 1 else 'single',
+        },
+        'roofline': roof,
+        'kernels': kernels,
+        'cpu_baseline': cpu,
+    }
+    print(json.dumps(line))
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

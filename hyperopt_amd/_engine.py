@@ -28,6 +28,7 @@ TPE_E_INDEX = -7
 GMM, LGMM, CAT = 0, 1, 2
 HAS_LOW, HAS_HIGH, HAS_Q, PCHOICE = 1, 2, 4, 8
 OBS_IDENT, OBS_LOG, OBS_LOG_CLIP_EXPLOW, OBS_LOG_CLIP_EPS = 0, 1, 2, 3
+KIND_NAMES = ('lse_gmm', 'lse_lgmm', 'erf_gmm', 'erf_lgmm', 'categorical')
 
 # every symbol include/tpe_engine.h declares (checked by tests)
 EXPORTS = (
@@ -36,6 +37,7 @@ EXPORTS = (
     'tpe_lpdf', 'tpe_score', 'tpe_sample', 'tpe_plan_create', 'tpe_plan_destroy',
     'tpe_plan_num_levels', 'tpe_plan_set_history', 'tpe_plan_fit', 'tpe_plan_get_mixture',
     'tpe_plan_suggest', 'tpe_plan_merge', 'tpe_plan_score_candidates', 'tpe_plan_last_stats',
+    'tpe_plan_profile', 'tpe_plan_profile_read', 'tpe_microbench',
 )
 
 
@@ -69,6 +71,29 @@ _lib = None
 _lib_lock = threading.Lock()
 
 
+def _share_hip_runtime():
+    """Make the engine and PyTorch use ONE HIP runtime.
+
+    libtpe_engine.so needs ``libamdhip64.so.7``; PyTorch-ROCm ships its own
+    copy (same soname) and loads it by file name.  Whichever loads second
+    would bring a second runtime into the process, and the second one sees no
+    GPU.  Pre-loading torch's copy (without importing torch) makes the engine
+    bind to it, so torch tensors and engine launches share one runtime.
+    TPE_ENGINE_HIP_RUNTIME=system keeps /opt/rocm's runtime instead."""
+    if os.environ.get('TPE_ENGINE_HIP_RUNTIME', '') == 'system':
+        return
+    import importlib.util
+    try:
+        spec = importlib.util.find_spec('torch')
+    except (ImportError, ValueError):
+        spec = None
+    if spec is None or not spec.origin:
+        return
+    hip = os.path.join(os.path.dirname(spec.origin), 'lib', 'libamdhip64.so')
+    if os.path.exists(hip):
+        C.CDLL(hip, mode=C.RTLD_GLOBAL)
+
+
 def load_library(path: str = LIB_PATH):
     """Load libtpe_engine.so and declare its signatures (no device needed)."""
     global _lib
@@ -79,6 +104,7 @@ def load_library(path: str = LIB_PATH):
             raise EngineUnavailable(
                 'libtpe_engine.so not found at %s: build it with `make -C '
                 'hyperopt_amd/csrc` or __graft_entry__.build()' % path)
+        _share_hip_runtime()
         lib = C.CDLL(path)
         vp, i32, i64, u32, u64, dbl = C.c_void_p, C.c_int32, C.c_int64, C.c_uint32, C.c_uint64, C.c_double
         sig = {
@@ -106,6 +132,9 @@ def load_library(path: str = LIB_PATH):
             'tpe_plan_merge': (C.c_int, [vp, vp, i32, i32, vp, i32, vp]),
             'tpe_plan_score_candidates': (C.c_int, [vp, i32, _D, i64, _D, _D, C.POINTER(i64), _D]),
             'tpe_plan_last_stats': (C.c_int, [vp, _D, _D]),
+            'tpe_plan_profile': (C.c_int, [vp, i32]),
+            'tpe_plan_profile_read': (C.c_int, [vp, i32, _D, C.POINTER(i64), _D]),
+            'tpe_microbench': (C.c_int, [vp, i32, _D]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -165,6 +194,12 @@ class Engine(object):
         if rc == TPE_E_INVALID:
             raise ValueError(msg)
         raise EngineError('TPE engine error %d: %s' % (rc, msg))
+
+    def microbench(self, which):
+        r = C.c_double(0)
+        with self.lock:
+            self.check(self.lib.tpe_microbench(self.h, int(which), C.byref(r)))
+        return r.value
 
     # -- operator level ----------------------------------------------------
     def split(self, losses, gamma, gamma_cap=25):
@@ -367,6 +402,20 @@ class Plan(object):
             e.check(e.lib.tpe_plan_score_candidates(self.p, int(hp), _dp(x), x.size, _dp(lb),
                                                     _dp(la), C.byref(bi), C.byref(bs)))
         return lb, la, bi.value, bs.value
+
+    def profile(self, capacity):
+        e = self.engine
+        with e.lock:
+            e.check(e.lib.tpe_plan_profile(self.p, int(capacity)))
+
+    def profile_read(self, kind):
+        """(avg_ms, launches, pairs_per_launch) of one scoring kind."""
+        e = self.engine
+        ms, n, pairs = C.c_double(0), C.c_int64(0), C.c_double(0)
+        with e.lock:
+            e.check(e.lib.tpe_plan_profile_read(self.p, int(kind), C.byref(ms), C.byref(n),
+                                                C.byref(pairs)))
+        return ms.value, n.value, pairs.value
 
     def last_stats(self):
         e = self.engine

@@ -56,6 +56,14 @@ struct tpe_plan {
   double *d_cand = nullptr;
   size_t cand_cap = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // per-kind event ring around every scoring launch (tpe_plan_profile)
+  struct Prof {
+    std::vector<hipEvent_t> a, b;
+    std::vector<double> pairs;  // candidate-component pairs the launch covers
+    int64_t n = 0;
+  };
+  Prof prof[KIND_CAT + 1];
+  int32_t prof_cap = 0;
   bool timed = false;
   int64_t last_ncand = 0, last_nsug = 0;
   int32_t last_level = -1;
@@ -99,6 +107,11 @@ void plan_free_buffers(tpe_plan *p) {
   for (void *b : bufs) dfree(b);
   if (p->ev0) (void)hipEventDestroy(p->ev0);
   if (p->ev1) (void)hipEventDestroy(p->ev1);
+  for (auto &pr : p->prof) {
+    for (auto e : pr.a) (void)hipEventDestroy(e);
+    for (auto e : pr.b) (void)hipEventDestroy(e);
+    pr.a.clear(); pr.b.clear(); pr.pairs.clear(); pr.n = 0;
+  }
 }
 
 int validate_space(tpe_engine *h, const tpe_space *sp) {
@@ -289,6 +302,13 @@ int ensure_cand(tpe_engine *h, tpe_plan *p, size_t n) {
   return TPE_OK;
 }
 
+// Pairs a scoring launch evaluates if every hp of the group is active: uses
+// the host copy of the mixture sizes refreshed by tpe_plan_profile_read.
+double group_pairs(tpe_plan *p, int kind, int32_t n_slots, int64_t cn, int64_t n_sug) {
+  (void)p; (void)kind; (void)n_slots;
+  return (double)cn * (double)n_sug;  // x (K_b + K_a) applied at read time
+}
+
 // One (level, kind) group: draw candidates (unless external), score, reduce.
 // Candidates are processed in chunks so the buffer stays <= 512 MB.
 int run_group(tpe_engine *h, tpe_plan *p, int32_t kind, const int32_t *level_hps_dev,
@@ -339,7 +359,18 @@ int run_group(tpe_engine *h, tpe_plan *p, int32_t kind, const int32_t *level_hps
       a.cand = p->d_cand;
       CKH(launch_draw(a, st));
     }
+    tpe_plan::Prof *pr = nullptr;
+    if (p->prof_cap > 0 && !ext) {
+      pr = &p->prof[kind];
+      if (pr->n >= p->prof_cap) pr = nullptr;  // ring full: stop recording
+    }
+    if (pr) CKH(hipEventRecord(pr->a[pr->n], st));
     CKH(launch_score(a, kind, grid_x, st));
+    if (pr) {
+      CKH(hipEventRecord(pr->b[pr->n], st));
+      pr->pairs[pr->n] = group_pairs(p, kind, n_slots, cn, n_sug);
+      pr->n++;
+    }
     CKH(launch_reduce(level_hps_dev, n_slots, (int32_t)n_sug, p->P, grid_x, c0 > 0 ? 1 : 0,
                       p->d_partial, p->d_results, st));
     c0 += cn;
@@ -795,6 +826,91 @@ int tpe_plan_score_candidates(tpe_plan_t p, int32_t hp, const double *x, int64_t
   CKH(hipStreamSynchronize(st));
   if (best_index) *best_index = r.index;
   if (best_score) *best_score = r.score;
+  return TPE_OK;
+}
+
+int tpe_plan_profile(tpe_plan_t p, int32_t capacity) {
+  if (!p || capacity < 0) return TPE_E_INVALID;
+  tpe_engine *h = p->eng;
+  CKH(hipSetDevice(h->device));
+  CKH(hipDeviceSynchronize());
+  for (auto &pr : p->prof) {
+    for (auto e : pr.a) (void)hipEventDestroy(e);
+    for (auto e : pr.b) (void)hipEventDestroy(e);
+    pr.a.assign(capacity, nullptr);
+    pr.b.assign(capacity, nullptr);
+    pr.pairs.assign(capacity, 0.0);
+    pr.n = 0;
+    for (int i = 0; i < capacity; ++i) {
+      CKH(hipEventCreate(&pr.a[i]));
+      CKH(hipEventCreate(&pr.b[i]));
+    }
+  }
+  p->prof_cap = capacity;
+  return TPE_OK;
+}
+
+int tpe_plan_profile_read(tpe_plan_t p, int32_t kind, double *avg_ms, int64_t *launches,
+                          double *pairs_per_launch) {
+  if (!p || kind < 0 || kind > KIND_CAT) return TPE_E_INVALID;
+  tpe_engine *h = p->eng;
+  CKH(hipSetDevice(h->device));
+  CKH(hipDeviceSynchronize());
+  auto &pr = p->prof[kind];
+  double tot = 0.0, pairs = 0.0;
+  // components per candidate of the kind's hps (all levels), active in the
+  // last suggestion (levels' activity is the same for every profiled step)
+  std::vector<MixInfo> info(2 * (size_t)p->P);
+  std::vector<Partial> res((size_t)std::max<int64_t>(1, p->last_nsug) * p->P);
+  CKH(hipMemcpy(info.data(), p->d_info, info.size() * sizeof(MixInfo), hipMemcpyDeviceToHost));
+  if (p->d_results)
+    CKH(hipMemcpy(res.data(), p->d_results, res.size() * sizeof(Partial), hipMemcpyDeviceToHost));
+  double kk = 0.0;  // sum over suggestions of active (K_b + K_a), per suggestion avg
+  for (int hp = 0; hp < p->P; ++hp) {
+    if (score_kind(p->hps[hp]) != kind || kind == KIND_CAT) continue;
+    double act = 0;
+    for (int64_t s = 0; s < std::max<int64_t>(1, p->last_nsug); ++s) act += res[s * p->P + hp].active;
+    act /= (double)std::max<int64_t>(1, p->last_nsug);
+    kk += act * ((double)info[2 * hp].K + info[2 * hp + 1].K);
+  }
+  for (int64_t i = 0; i < pr.n; ++i) {
+    float ms = 0.f;
+    CKH(hipEventElapsedTime(&ms, pr.a[i], pr.b[i]));
+    tot += ms;
+    pairs += pr.pairs[i] * kk;
+  }
+  if (avg_ms) *avg_ms = pr.n ? tot / pr.n : 0.0;
+  if (launches) *launches = pr.n;
+  if (pairs_per_launch) *pairs_per_launch = pr.n ? pairs / pr.n : 0.0;
+  pr.n = 0;
+  return TPE_OK;
+}
+
+int tpe_microbench(tpe_handle_t h, int32_t which, double *per_second) {
+  if (!h || !per_second || which < 0 || which > 2) return TPE_E_INVALID;
+  CKH(hipSetDevice(h->device));
+  hipDeviceProp_t prop;
+  CKH(hipGetDeviceProperties(&prop, h->device));
+  const int blocks = prop.multiProcessorCount * 8;
+  const int iters = which == 2 ? 256 : 4096;
+  double *sink = nullptr;
+  CKH(dalloc(&sink, (size_t)blocks * 256));
+  hipEvent_t a, b;
+  CKH(hipEventCreate(&a));
+  CKH(hipEventCreate(&b));
+  CKH(launch_micro(which, blocks, iters, sink, h->stream));  // warm-up
+  CKH(hipEventRecord(a, h->stream));
+  for (int r = 0; r < 4; ++r) CKH(launch_micro(which, blocks, iters, sink, h->stream));
+  CKH(hipEventRecord(b, h->stream));
+  CKH(hipEventSynchronize(b));
+  float ms = 0.f;
+  CKH(hipEventElapsedTime(&ms, a, b));
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  dfree(sink);
+  const double chains = which == 2 ? 4.0 : 8.0;
+  const double per_op = which == 1 ? 2.0 : 1.0;  // FMA = 2 flops
+  *per_second = 4.0 * blocks * 256.0 * iters * chains * per_op / (ms * 1e-3);
   return TPE_OK;
 }
 

@@ -101,4 +101,6 @@ hipError_t launch_sample(const tpe_hp *hp_dev, const double *mw,
                          int64_t offset, int64_t n, double *out,
                          hipStream_t st);
 
+hipError_t launch_micro(int which, int blocks, int iters, double *sink, hipStream_t st);
+
 }  // namespace tpe

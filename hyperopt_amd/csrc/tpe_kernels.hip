@@ -845,6 +845,61 @@ __global__ __launch_bounds__(256) void k_sample(const tpe_hp *__restrict__ hpd,
 }
 
 // ------------------------------------------------------------------------
+// register-only microkernels for the roofline (tpe_microbench)
+// ------------------------------------------------------------------------
+template <int WHICH>
+__global__ __launch_bounds__(256) void k_micro(int iters, double *sink) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if constexpr (WHICH == 0) {  // v_exp_f32 throughput, 8 independent chains
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = 0.001f * (t + j);
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = __builtin_amdgcn_exp2f(-v[j]);
+    }
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += v[j];
+    if (acc == 12345.f) sink[t] = acc;
+  } else if constexpr (WHICH == 1) {  // fp64 FMA throughput, 8 chains
+    double v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = 1e-3 * (t + j);
+    const double b = 0.999999, c = 1e-7;
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = fma(v[j], b, c);
+    }
+    double acc = 0.0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += v[j];
+    if (acc == 12345.0) sink[t] = acc;
+  } else {  // OCML fp64 erf throughput, 4 chains
+    double v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = 1e-3 * (t + j);
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = erf(v[j]) - 0.25;
+    }
+    double acc = 0.0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc += v[j];
+    if (acc == 12345.0) sink[t] = acc;
+  }
+}
+
+hipError_t launch_micro(int which, int blocks, int iters, double *sink, hipStream_t st) {
+  switch (which) {
+    case 0: k_micro<0><<<blocks, 256, 0, st>>>(iters, sink); break;
+    case 1: k_micro<1><<<blocks, 256, 0, st>>>(iters, sink); break;
+    default: k_micro<2><<<blocks, 256, 0, st>>>(iters, sink); break;
+  }
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------
 // launch wrappers
 // ------------------------------------------------------------------------
 hipError_t launch_split(const double *losses, int64_t n, int32_t n_below, uint8_t *below,

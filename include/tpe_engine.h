@@ -190,6 +190,18 @@ int tpe_plan_score_candidates(tpe_plan_t p, int32_t hp, const double *x,
  * they evaluated.                                                          */
 int tpe_plan_last_stats(tpe_plan_t p, double *score_ms, double *pairs);
 
+/* Per-kernel profiling: record HIP events around every scoring launch of the
+ * next `capacity` launches per lpdf kind (0: off), then read the average
+ * device duration and the (candidate, component) pairs per launch of one
+ * kind (0 LSE-GMM, 1 LSE-LGMM, 2 ERF-GMM, 3 ERF-LGMM, 4 categorical).     */
+int tpe_plan_profile(tpe_plan_t p, int32_t capacity);
+int tpe_plan_profile_read(tpe_plan_t p, int32_t kind, double *avg_ms,
+                          int64_t *launches, double *pairs_per_launch);
+
+/* Register-only microbenchmarks for the roofline: which = 0 v_exp_f32
+ * (results/s), 1 fp64 FMA (flop/s), 2 OCML fp64 erf (results/s).          */
+int tpe_microbench(tpe_handle_t h, int32_t which, double *per_second);
+
 #ifdef __cplusplus
 }
 #endif

@@ -409,14 +409,30 @@ def hp_order(hps):
     def visit(lab):
         if lab in done:
             return
-        for parent, _ in hps[lab]['conds']:
-            visit(parent)
+        for path in _paths(hps[lab]):
+            for parent, _ in path:
+                visit(parent)
         done.add(lab)
         order.append(lab)
 
     for lab in sorted(hps, reverse=True):
         visit(lab)
     return order
+
+
+def _paths(h):
+    """Alternative condition paths of a hp: ``paths`` (list of tuples of
+    (parent, branch)) or the single path ``conds``."""
+    if 'paths' in h:
+        return h['paths']
+    return [h['conds']]
+
+
+def is_active(h, chosen):
+    for path in _paths(h):
+        if all(chosen.get(p) is not None and int(chosen[p]) == b for p, b in path):
+            return True
+    return False
 
 
 def suggest_reference_stream(hps, loss_tids, losses, obs, seed, n_ei=24,
@@ -429,7 +445,7 @@ def suggest_reference_stream(hps, loss_tids, losses, obs, seed, n_ei=24,
     chosen, detail = {}, {}
     for lab in hp_order(hps):
         h = hps[lab]
-        active = all(chosen.get(p) == b for p, b in h['conds'])
+        active = is_active(h, chosen)
         n = n_ei if active else 0
         o_tids, o_vals = obs[lab]
         bo, ao = split_observations(o_tids, o_vals, loss_tids, losses, gamma, kind=kind)

@@ -17,6 +17,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REF = sys.argv[1] if len(sys.argv) > 1 else '/tmp/oracle'
+ONLY = sys.argv[2:]  # optional subset of generator names, e.g. testopt
 sys.path.insert(0, REF)
 sys.path.insert(0, os.path.dirname(HERE))          # tests/ for spaces.py
 
@@ -345,12 +346,36 @@ def gen_suggest():
         json.dump(meta, f, indent=1)
 
 
+# ---------------------------------------------------------------- TestOpt runs
+def gen_testopt():
+    """fmin trajectories of the reference's TestOpt (test_tpe.py:517-641)."""
+    from functools import partial
+    from hyperopt.pyll import as_apply
+    import domains
+    out = {}
+    for name in domains.NAMES:
+        kw, n = domains.settings(name)
+        space = domains.build(name, hp, scope, as_apply)
+        old = np.seterr('raise')
+        np.seterr(under='ignore')
+        try:
+            t = Trials()
+            fmin(lambda x: x, space=space, algo=partial(tpe.suggest, **kw), trials=t,
+                 max_evals=n, rstate=np.random.RandomState(123))
+        finally:
+            np.seterr(**old)
+        vals = [{k: (v[0] if v else None) for k, v in tr['misc']['vals'].items()}
+                for tr in t.trials]
+        out[name] = dict(vals=vals, losses=t.losses(), min=min(t.losses()))
+        print('testopt', name, len(t.trials), min(t.losses()))
+    with open(os.path.join(HERE, 'testopt_traj.json'), 'w') as f:
+        json.dump(out, f)
+
+
 if __name__ == '__main__':
     np.seterr(all='ignore')
-    gen_split()
-    gen_parzen()
-    gen_lpdf()
-    gen_categorical()
-    gen_samplers()
-    gen_cfg1()
-    gen_suggest()
+    gens = dict(split=gen_split, parzen=gen_parzen, lpdf=gen_lpdf, categorical=gen_categorical,
+                samplers=gen_samplers, cfg1=gen_cfg1, suggest=gen_suggest, testopt=gen_testopt)
+    for name, g in gens.items():
+        if not ONLY or name in ONLY:
+            g()

@@ -132,3 +132,24 @@ def test_whole_suggest_reference_stream(name):
         np.testing.assert_array_equal(detail[lab]['cand'], unpack(d, 'samples', k))
         np.testing.assert_array_equal(detail[lab]['llik_b'], unpack(d, 'llik_b', k))
         np.testing.assert_array_equal(detail[lab]['llik_a'], unpack(d, 'llik_a', k))
+
+
+@pytest.mark.parametrize('name', ['branin', 'distractor', 'gauss_wave', 'gauss_wave2',
+                                  'many_dists', 'n_arms', 'q1_lognormal', 'quadratic1'])
+def test_oracle_fmin_trajectories_equal_reference(name):
+    """The oracle, driven through hyperopt_amd's fmin/Trials host layer,
+    replays the reference's TestOpt runs trial for trial (pins both the
+    oracle numerics and the host history/seeding semantics)."""
+    import functools
+    import hyperopt_amd as H
+    from hyperopt_amd import hp, Trials, fmin
+    from hyperopt_amd.expr import as_apply
+    import domains
+    from oracle_algo import oracle_suggest, trajectory
+    ref = load_json('testopt_traj.json')[name]
+    kw, n = domains.settings(name)
+    t = Trials()
+    fmin(lambda x: x, domains.build(name, hp, H.scope, as_apply),
+         algo=functools.partial(oracle_suggest, **kw), max_evals=n, trials=t,
+         rstate=np.random.RandomState(123))
+    assert trajectory(t) == ref['vals']
