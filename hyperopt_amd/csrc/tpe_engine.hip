@@ -54,6 +54,7 @@ struct tpe_plan {
   double *d_ext = nullptr, *d_lb = nullptr, *d_la = nullptr;
   size_t ext_cap = 0;
   double *d_cand = nullptr;
+  int32_t *d_cpos = nullptr;
   size_t cand_cap = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // per-kind event ring around every scoring launch (tpe_plan_profile)
@@ -103,7 +104,7 @@ void plan_free_buffers(tpe_plan *p) {
   void *bufs[] = {p->d_hps, p->d_cp, p->d_cb, p->d_level_hps, p->d_all_hps, p->d_pprior,
                   p->d_losses, p->d_vals, p->d_active, p->d_below, p->d_mw, p->d_mmu,
                   p->d_msig, p->d_scratch, p->d_info, p->d_coef, p->d_results, p->d_seeds,
-                  p->d_partial, p->d_ext, p->d_lb, p->d_la, p->d_cand};
+                  p->d_partial, p->d_ext, p->d_lb, p->d_la, p->d_cand, p->d_cpos};
   for (void *b : bufs) dfree(b);
   if (p->ev0) (void)hipEventDestroy(p->ev0);
   if (p->ev1) (void)hipEventDestroy(p->ev1);
@@ -276,27 +277,36 @@ int ensure_ext(tpe_engine *h, tpe_plan *p, size_t n) {
   return TPE_OK;
 }
 
-// component split + grid size for one level launch
-void choose_geometry(int64_t n_cand, int64_t n_slots, int64_t n_sug, int32_t &ks,
+// Component split (ks waves of a 16-wave block share 64 candidates) and grid
+// size for one scoring launch: aim for >= 8 waves per SIMD of the 1024 SIMDs
+// when the candidate count allows, else split the mixtures further.
+void choose_geometry(int64_t n_cand, int64_t n_slots, int64_t n_sug, int32_t kind, int32_t &ks,
                      int32_t &tiles, int32_t &grid_x) {
-  const int64_t target = 2048;  // ~8 workgroups per CU on 256 CUs
-  ks = 4;
-  for (int cand_ks : {1, 2, 4}) {
-    const int64_t tc = 64 * (4 / cand_ks);
-    const int64_t t = (n_cand + tc - 1) / tc;
-    if (t * n_slots * n_sug >= target || cand_ks == 4) { ks = cand_ks; break; }
+  const int64_t want_waves = 8192;
+  ks = 16;
+  if (kind != KIND_CAT) {
+    for (int c : {1, 2, 4, 8, 16}) {
+      const int64_t groups = (n_cand + 63) / 64;  // 64-candidate groups per (s, hp)
+      if (groups * n_slots * n_sug * c >= want_waves || c == 16) { ks = c; break; }
+    }
+  } else {
+    ks = 1;
   }
-  const int64_t tc = 64 * (4 / ks);
+  const int64_t tc = 64 * (16 / ks);
   tiles = (int32_t)std::max<int64_t>(0, (n_cand + tc - 1) / tc);
-  int64_t per = std::max<int64_t>(1, (target * 4) / std::max<int64_t>(1, n_slots * n_sug));
+  const int64_t target_blocks = 256 * 4;  // 1024-thread blocks, a few per CU in flight
+  int64_t per = std::max<int64_t>(1, target_blocks / std::max<int64_t>(1, n_slots * n_sug));
   grid_x = (int32_t)std::max<int64_t>(1, std::min<int64_t>(std::max(tiles, 1), per));
 }
 
 int ensure_cand(tpe_engine *h, tpe_plan *p, size_t n) {
   if (n > p->cand_cap) {
     dfree(p->d_cand);
+    dfree(p->d_cpos);
     p->d_cand = nullptr;
+    p->d_cpos = nullptr;
     CKH(dalloc(&p->d_cand, n));
+    CKH(dalloc(&p->d_cpos, n));
     p->cand_cap = n;
   }
   return TPE_OK;
@@ -341,7 +351,7 @@ int run_group(tpe_engine *h, tpe_plan *p, int32_t kind, const int32_t *level_hps
   do {
     const int64_t cn = std::min(chunk, n_cand - c0);
     int32_t ks, tiles, grid_x;
-    choose_geometry(cn, n_slots, n_sug, ks, tiles, grid_x);
+    choose_geometry(cn, n_slots, n_sug, kind, ks, tiles, grid_x);
     int rc = ensure_suggest_state(h, p, n_sug, (size_t)n_sug * n_slots * grid_x);
     if (rc) return rc;
     a.partial = p->d_partial;
@@ -351,6 +361,7 @@ int run_group(tpe_engine *h, tpe_plan *p, int32_t kind, const int32_t *level_hps
     a.cand_begin = cand_begin + c0;
     a.ks = ks;
     a.tiles = tiles;
+    a.cand_pos = nullptr;
     if (ext) {
       a.cand = ext;
     } else {
@@ -358,6 +369,10 @@ int run_group(tpe_engine *h, tpe_plan *p, int32_t kind, const int32_t *level_hps
       if (rc) return rc;
       a.cand = p->d_cand;
       CKH(launch_draw(a, st));
+      if (kind == KIND_ERF_G || kind == KIND_ERF_L) {  // wave-coherent erf skipping
+        CKH(launch_sort_cand(a, p->d_cpos, st));
+        a.cand_pos = p->d_cpos;
+      }
     }
     tpe_plan::Prof *pr = nullptr;
     if (p->prof_cap > 0 && !ext) {

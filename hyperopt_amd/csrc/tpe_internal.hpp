@@ -59,6 +59,7 @@ struct ScoreArgs {
   const double *mw, *mmu, *msig;  // [2*P][kcap] (sampler reads side 0)
   const uint64_t *seeds;     // [S]
   const double *cand;        // candidates [S][n_slots][n_cand] (drawn or external)
+  const int32_t *cand_pos;   // optional: original position of each (sorted) candidate
   double *out_lb, *out_la;   // optional per-candidate lliks (ext only)
   Partial *results;          // [S][P]
   Partial *partial;          // [S][n_slots][grid.x]
@@ -87,6 +88,7 @@ hipError_t launch_prep(const tpe_hp *hps, int32_t n_hp, const double *mw,
                        hipStream_t st);
 hipError_t launch_score(const ScoreArgs &a, int32_t kind, int32_t grid_x, hipStream_t st);
 hipError_t launch_draw(const ScoreArgs &a, hipStream_t st);
+hipError_t launch_sort_cand(const ScoreArgs &a, int32_t *pos_out, hipStream_t st);
 hipError_t launch_reduce(const int32_t *level_hps, int32_t n_slots,
                          int32_t n_suggest, int32_t n_hp, int32_t grid_x,
                          int32_t accumulate, const Partial *partial,

@@ -168,6 +168,45 @@ __device__ T block_sum_i(T v, T *buf) {
 }
 
 // ------------------------------------------------------------------------
+// Block-wide bitonic sort of (key, position) pairs in LDS, ascending in the
+// total order "numpy argsort with NaN last, ties by position" (stable).
+// np2 = power of two >= n; slots [n, np2) are padded with (NaN, INT_MAX).
+// ------------------------------------------------------------------------
+constexpr int kSortMax = 8192;  // 8192 x (8 + 4) B = 96 KB of LDS
+
+__device__ __forceinline__ bool key_less(double a, int64_t ia, double b, int64_t ib);
+
+__device__ void block_bitonic_sort(double *key, int *pos, int n, int np2) {
+  for (int i = n + threadIdx.x; i < np2; i += blockDim.x) {
+    key[i] = NAN;
+    pos[i] = 0x7fffffff;
+  }
+  __syncthreads();
+  for (int k = 2; k <= np2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int t = threadIdx.x; t < (np2 >> 1); t += blockDim.x) {
+        const int i = 2 * t - (t & (j - 1));
+        const int l = i + j;
+        const bool up = (i & k) == 0;
+        const double ki = key[i], kl = key[l];
+        const int pi = pos[i], pl = pos[l];
+        if (key_less(kl, pl, ki, pi) == up) {
+          key[i] = kl; key[l] = ki;
+          pos[i] = pl; pos[l] = pi;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+__device__ __forceinline__ int pow2_at_least(int n) {
+  int p = 2;
+  while (p < n) p <<= 1;
+  return p;
+}
+
+// ------------------------------------------------------------------------
 // (a2) split: mark the n_below lowest losses.  Key order = numpy argsort with
 // NaN last; ties by position (stable).  One block, n_below <= 25 rounds of a
 // block-wide argmin (top-k with k <= 25).
@@ -183,10 +222,20 @@ __device__ __forceinline__ bool key_less(double a, int64_t ia, double b,
 __global__ __launch_bounds__(1024) void k_split(const double *__restrict__ losses,
                                                 int64_t n, int32_t n_below,
                                                 uint8_t *__restrict__ below) {
+  extern __shared__ __attribute__((aligned(16))) double dyn_lds[];
   __shared__ double sv[16];
   __shared__ int64_t si[16];
   for (int64_t j = threadIdx.x; j < n; j += blockDim.x) below[j] = 0;
   __syncthreads();
+  if (n <= kSortMax) {  // one LDS sort, then the first n_below are "good"
+    double *key = dyn_lds;
+    int *pos = reinterpret_cast<int *>(dyn_lds + kSortMax);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) { key[i] = losses[i]; pos[i] = i; }
+    __syncthreads();
+    block_bitonic_sort(key, pos, (int)n, pow2_at_least((int)n));
+    for (int r = threadIdx.x; r < n_below && r < n; r += blockDim.x) below[pos[r]] = 1;
+    return;
+  }
   // previous winner (strict lower bound of remaining keys)
   double pv = -INFINITY;
   int64_t pi = -1;
@@ -290,10 +339,12 @@ __global__ __launch_bounds__(1024) void k_fit(
     m += tot;
   }
   __syncthreads();
-  // cache in LDS when it fits (dynamic size chosen by the launcher)
+  // LDS layout (96 KB): m <= kSortMax -> key[8192] f64 + pos[8192] i32;
+  // otherwise an LDS copy of the observations when <= 12288 of them fit.
+  const bool small = m <= kSortMax;
   double *sob = dyn_lds;
-  const bool use_lds = (int64_t)m * 8 <= (int64_t)(96 * 1024);
-  if (use_lds) {
+  int *spos = reinterpret_cast<int *>(dyn_lds + kSortMax);
+  if (m <= 12288) {
     for (int i = threadIdx.x; i < m; i += blockDim.x) sob[i] = ob[i];
     __syncthreads();
   } else {
@@ -301,12 +352,26 @@ __global__ __launch_bounds__(1024) void k_fit(
   }
 
   if (H.family == TPE_CAT) {
-    // LF-weighted bincount in observation order (np.bincount) + pseudocounts
+    // LF-weighted bincount in observation order (np.bincount) + pseudocounts.
+    // Weights precomputed in parallel (LDS) so each bin's serial sum -- kept
+    // serial for bit-identical rounding -- is a short dependent chain.
     const int upper = H.upper;
+    if (small) {
+      for (int i = threadIdx.x; i < m; i += blockDim.x) {
+        spos[i] = (int)sob[i];
+        sob[i] = lf_weight(i, m, lf);
+      }
+      __syncthreads();
+    }
     for (int c = threadIdx.x; c < upper; c += blockDim.x) {
       double cnt = 0.0;
-      for (int i = 0; i < m; ++i)
-        if ((int64_t)sob[i] == c) cnt += lf_weight(i, m, lf);
+      if (small) {
+        for (int i = 0; i < m; ++i)
+          if (spos[i] == c) cnt += sob[i];
+      } else {
+        for (int i = 0; i < m; ++i)
+          if ((int64_t)sob[i] == c) cnt += lf_weight(i, m, lf);
+      }
       double pc;
       if (H.flags & TPE_PCHOICE)
         pc = cnt + (double)upper * (prior_weight * pprior[H.pprior_begin + c]);
@@ -345,8 +410,19 @@ __global__ __launch_bounds__(1024) void k_fit(
     for (int i = threadIdx.x; i < m; i += blockDim.x) cl += (sob[i] < pm) ? 1 : 0;
     pos = block_sum_i<int>(cl, sm.wsum);
     const bool lfw = lf && lf < m;
-    // rank by counting (stable; 4 elements per pass share each LDS read)
-    for (int i0 = threadIdx.x; i0 < m; i0 += 4 * blockDim.x) {
+    if (small) {
+      // stable LDS bitonic sort; sorted slot r goes to r + (r >= prior_pos)
+      for (int i = threadIdx.x; i < m; i += blockDim.x) spos[i] = i;
+      __syncthreads();
+      block_bitonic_sort(sob, spos, m, pow2_at_least(m));
+      for (int r = threadIdx.x; r < m; r += blockDim.x) {
+        const int o = r + (r >= pos ? 1 : 0);
+        mu[o] = sob[r];
+        w[o] = lfw ? lf_weight(spos[r], m, lf) : 1.0;
+      }
+    }
+    // large m: rank by counting (stable; 4 elements per pass share each read)
+    for (int i0 = threadIdx.x; i0 < (small ? 0 : m); i0 += 4 * blockDim.x) {
       int idx[4];
       double vi[4];
       int rk[4];
@@ -556,18 +632,18 @@ __device__ double draw_one(const tpe_hp &H, const MixInfo &I,
 // log-sum-exp slice in log2 units: m = max_k t_k, s = sum_k 2^(t_k - m),
 // t_k = c_k - ((y - mu_k) a_k)^2.  Exponent arguments and the accumulator are
 // fp64; 2^(t-m) in [0,1] is one v_exp_f32 (rel. err ~1e-7 per term).
-__device__ __forceinline__ void lse_slice(const Coef *__restrict__ c, int k0, int k1,
+__device__ __forceinline__ void lse_slice(const Coef *__restrict__ c, int k0, int k1, int ks,
                                           double y, double &m_out, double &s_out) {
   double m = -INFINITY;
 #pragma unroll 4
-  for (int k = k0; k < k1; ++k) {
+  for (int k = k0; k < k1; k += ks) {
     const double z = (y - c[k].x) * c[k].y;
     m = fmax(m, fma(-z, z, c[k].z));
   }
   double s = 0.0;
   if (m != -INFINITY || !(fabs(y) < INFINITY)) {
 #pragma unroll 4
-    for (int k = k0; k < k1; ++k) {
+    for (int k = k0; k < k1; k += ks) {
       const double z = (y - c[k].x) * c[k].y;
       const double t = fma(-z, z, c[k].z);
       s += (double)__builtin_amdgcn_exp2f((float)(t - m));
@@ -582,10 +658,10 @@ __device__ __forceinline__ void lse_slice(const Coef *__restrict__ c, int k0, in
 // exact 0 in float64 (erf saturates to +-1), so they are skipped.
 template <bool LOGN>
 __device__ __forceinline__ double erf_slice(const Coef *__restrict__ c, int k0,
-                                            int k1, double ub, double lb) {
+                                            int k1, int ks, double ub, double lb) {
 #pragma clang fp contract(off)
   double prob = 0.0;
-  for (int k = k0; k < k1; ++k) {
+  for (int k = k0; k < k1; k += ks) {
     const double zu = (ub - c[k].x) * c[k].y;
     const double zl = (lb - c[k].x) * c[k].y;
     const bool dead = (zu >= 6.5 && zl >= 6.5) || (zu <= -6.5 && zl <= -6.5);
@@ -660,21 +736,51 @@ __global__ __launch_bounds__(256) void k_draw(ScoreArgs A) {
     out[li] = draw_one(H, ib, bw, bmu, bsg, seed, (uint64_t)(A.cand_begin + li), (uint32_t)hp);
 }
 
+// Sort each 8192-candidate chunk of every (suggestion, hp) by value, keeping
+// the original position: a wave then holds 64 neighbouring candidates, so a
+// mixture component far from all of them (erf saturated, exp underflowed)
+// is skipped by the whole wave.  Scores and argmax tie-breaks still use the
+// original global candidate index.
+__global__ __launch_bounds__(1024) void k_sort_cand(ScoreArgs A, int32_t *__restrict__ pos_out) {
+  extern __shared__ __attribute__((aligned(16))) double dyn_lds[];
+  const int slot = blockIdx.y, s = blockIdx.z;
+  const int hp = A.level_hps[slot];
+  if (!A.force_active &&
+      !hp_active(A.hps[hp], A.results + (int64_t)s * A.n_hp, A.cond_parent, A.cond_branch))
+    return;
+  const int64_t base = (int64_t)blockIdx.x * kSortMax;
+  if (base >= A.n_cand) return;
+  const int n = (int)min<int64_t>(kSortMax, A.n_cand - base);
+  double *cand = const_cast<double *>(A.cand) + ((int64_t)s * A.n_slots + slot) * A.n_cand + base;
+  int32_t *po = pos_out + ((int64_t)s * A.n_slots + slot) * A.n_cand + base;
+  double *key = dyn_lds;
+  int *pos = reinterpret_cast<int *>(dyn_lds + kSortMax);
+  for (int i = threadIdx.x; i < n; i += blockDim.x) { key[i] = cand[i]; pos[i] = i; }
+  __syncthreads();
+  block_bitonic_sort(key, pos, n, pow2_at_least(n));
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    cand[i] = key[i];
+    po[i] = (int32_t)(base + pos[i]);
+  }
+}
+
 // Scoring kernel, one instantiation per lpdf kind so each keeps its own
 // register budget (the erf path must not cap the log-sum-exp path's
 // occupancy).  grid = (candidate-tile blocks, hps of the group, suggestions);
 // 4 waves per block; with ks > 1 the waves of a 64-candidate group split the
 // components and combine their partial sums through LDS.
+constexpr int kScoreWaves = 16;  // 1024-thread scoring blocks
+
 template <int KIND>
-__global__ __launch_bounds__(256) void k_score(ScoreArgs A, const Coef *__restrict__ coef,
+__global__ __launch_bounds__(1024) void k_score(ScoreArgs A, const Coef *__restrict__ coef,
                                                const double *__restrict__ cand_all) {
   constexpr bool LSE = KIND == KIND_LSE_G || KIND == KIND_LSE_L;
   constexpr bool ERF = KIND == KIND_ERF_G || KIND == KIND_ERF_L;
   constexpr bool CAT = KIND == KIND_CAT;
   constexpr bool LOGN = KIND == KIND_LSE_L || KIND == KIND_ERF_L;
-  __shared__ double red[4][4][64];
-  __shared__ double bs[4], bv[4];
-  __shared__ int64_t bi[4];
+  __shared__ double red[kScoreWaves][4][64];
+  __shared__ double bs[kScoreWaves], bv[kScoreWaves];
+  __shared__ int64_t bi[kScoreWaves];
   const int slot = blockIdx.y, s = blockIdx.z;
   const int hp = A.level_hps[slot];
   const tpe_hp H = A.hps[hp];
@@ -691,18 +797,18 @@ __global__ __launch_bounds__(256) void k_score(ScoreArgs A, const Coef *__restri
   const Coef *__restrict__ cb = coef + sb * A.kcap;
   const Coef *__restrict__ ca = coef + sa * A.kcap;
   const double *__restrict__ cand = cand_all + ((int64_t)s * A.n_slots + slot) * A.n_cand;
+  const int32_t *__restrict__ cpos =
+      A.cand_pos ? A.cand_pos + ((int64_t)s * A.n_slots + slot) * A.n_cand : nullptr;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int ks = A.ks, groups = 4 / ks;
+  const int ks = A.ks, groups = kScoreWaves / ks;
   const int grp = wave / ks, kp = wave % ks;
   const int TC = 64 * groups;
-  int kb0 = 0, kb1 = 0, ka0 = 0, ka1 = 0;
-  slice_bounds(ib.K, kp, ks, kb0, kb1);
-  slice_bounds(ia.K, kp, ks, ka0, ka1);
-  // wave-uniform component ranges -> scalar (SGPR) component loads
-  kb0 = __builtin_amdgcn_readfirstlane(kb0);
-  kb1 = __builtin_amdgcn_readfirstlane(kb1);
-  ka0 = __builtin_amdgcn_readfirstlane(ka0);
-  ka1 = __builtin_amdgcn_readfirstlane(ka1);
+  // wave kp of a candidate group takes components kp, kp+ks, ... (strided, so
+  // the live components of sorted candidates spread over the group's waves);
+  // wave-uniform bounds -> scalar (SGPR) component loads
+  const int kb0 = __builtin_amdgcn_readfirstlane(kp), kb1 = __builtin_amdgcn_readfirstlane(ib.K);
+  const int ka0 = kb0, ka1 = __builtin_amdgcn_readfirstlane(ia.K);
+  const int kst = __builtin_amdgcn_readfirstlane(ks);
 
   double best_s = NAN, best_v = NAN;
   int64_t best_i = -1;
@@ -713,8 +819,8 @@ __global__ __launch_bounds__(256) void k_score(ScoreArgs A, const Coef *__restri
     double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
     if constexpr (LSE) {
       const double y = LOGN ? log(x) : x;
-      lse_slice(cb, kb0, kb1, y, p0, p1);
-      lse_slice(ca, ka0, ka1, y, p2, p3);
+      lse_slice(cb, kb0, kb1, kst, y, p0, p1);
+      lse_slice(ca, ka0, ka1, kst, y, p2, p3);
     } else if constexpr (ERF) {
       const double hq = H.q / 2.0;
       double ub, lb;
@@ -728,8 +834,8 @@ __global__ __launch_bounds__(256) void k_score(ScoreArgs A, const Coef *__restri
         ub = u < 0.0 ? NAN : log(np_maximum(u, kEPS));
         lb = log(np_maximum(l, kEPS));
       }
-      p0 = erf_slice<LOGN>(cb, kb0, kb1, ub, lb);
-      p2 = erf_slice<LOGN>(ca, ka0, ka1, ub, lb);
+      p0 = erf_slice<LOGN>(cb, kb0, kb1, kst, ub, lb);
+      p2 = erf_slice<LOGN>(ca, ka0, ka1, kst, ub, lb);
     }
     if (!CAT && ks > 1) {
       red[wave][0][lane] = p0; red[wave][1][lane] = p1;
@@ -767,9 +873,10 @@ __global__ __launch_bounds__(256) void k_score(ScoreArgs A, const Coef *__restri
         lpb = in ? cb[c].x : NAN;
         lpa = in ? ca[c].x : NAN;
       }
-      if (A.out_lb) A.out_lb[li] = lpb;
-      if (A.out_la) A.out_la[li] = lpa;
-      const int64_t gi = A.cand_begin + li;
+      const int64_t lo = cpos ? (int64_t)cpos[li] : li;   // original position
+      if (A.out_lb) A.out_lb[lo] = lpb;
+      if (A.out_la) A.out_la[lo] = lpa;
+      const int64_t gi = A.cand_begin + lo;
       const double sc = lpb - lpa;
       if (better(sc, gi, best_s, best_i)) { best_s = sc; best_v = x; best_i = gi; }
     }
@@ -779,7 +886,7 @@ __global__ __launch_bounds__(256) void k_score(ScoreArgs A, const Coef *__restri
   if (lane == 0) { bs[wave] = best_s; bv[wave] = best_v; bi[wave] = best_i; }
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (int w = 1; w < 4; ++w)
+    for (int w = 1; w < kScoreWaves; ++w)
       if (better(bs[w], bi[w], best_s, best_i)) { best_s = bs[w]; best_v = bv[w]; best_i = bi[w]; }
     *pout = Partial{best_s, best_v, best_i, 1, 0};
   }
@@ -904,7 +1011,8 @@ hipError_t launch_micro(int which, int blocks, int iters, double *sink, hipStrea
 // ------------------------------------------------------------------------
 hipError_t launch_split(const double *losses, int64_t n, int32_t n_below, uint8_t *below,
                         hipStream_t st) {
-  k_split<<<1, 1024, 0, st>>>(losses, n, n_below, below);
+  const size_t lds = n <= kSortMax ? (size_t)kSortMax * 12 : 0;
+  k_split<<<1, 1024, lds, st>>>(losses, n, n_below, below);
   return hipGetLastError();
 }
 
@@ -914,7 +1022,7 @@ hipError_t launch_fit(const tpe_hp *hps, int32_t n_hp, const double *vals,
                       double *mmu, double *msig, MixInfo *info, int64_t kcap,
                       double *scratch, hipStream_t st) {
   if (n_hp <= 0) return hipSuccess;
-  const size_t lds = (size_t)(n < 12288 ? n : 12288) * 8;
+  const size_t lds = (size_t)12288 * 8;  // 96 KB: see the k_fit LDS layout
   k_fit<<<dim3(n_hp, 2), 1024, lds, st>>>(hps, vals, active, below, n, prior_weight, lf,
                                           pprior, mw, mmu, msig, info, kcap, scratch);
   return hipGetLastError();
@@ -933,11 +1041,11 @@ hipError_t launch_score(const ScoreArgs &a, int32_t kind, int32_t grid_x, hipStr
   if (a.n_suggest <= 0) return hipSuccess;
   const dim3 g(grid_x, a.n_slots, a.n_suggest);
   switch (kind) {
-    case KIND_LSE_G: k_score<KIND_LSE_G><<<g, 256, 0, st>>>(a, a.coef, a.cand); break;
-    case KIND_LSE_L: k_score<KIND_LSE_L><<<g, 256, 0, st>>>(a, a.coef, a.cand); break;
-    case KIND_ERF_G: k_score<KIND_ERF_G><<<g, 256, 0, st>>>(a, a.coef, a.cand); break;
-    case KIND_ERF_L: k_score<KIND_ERF_L><<<g, 256, 0, st>>>(a, a.coef, a.cand); break;
-    default: k_score<KIND_CAT><<<g, 256, 0, st>>>(a, a.coef, a.cand); break;
+    case KIND_LSE_G: k_score<KIND_LSE_G><<<g, 1024, 0, st>>>(a, a.coef, a.cand); break;
+    case KIND_LSE_L: k_score<KIND_LSE_L><<<g, 1024, 0, st>>>(a, a.coef, a.cand); break;
+    case KIND_ERF_G: k_score<KIND_ERF_G><<<g, 1024, 0, st>>>(a, a.coef, a.cand); break;
+    case KIND_ERF_L: k_score<KIND_ERF_L><<<g, 1024, 0, st>>>(a, a.coef, a.cand); break;
+    default: k_score<KIND_CAT><<<g, 1024, 0, st>>>(a, a.coef, a.cand); break;
   }
   return hipGetLastError();
 }
@@ -948,6 +1056,13 @@ hipError_t launch_draw(const ScoreArgs &a, hipStream_t st) {
   const int64_t cap = std::max<int64_t>(1, 8192 / ((int64_t)a.n_slots * a.n_suggest));
   const unsigned gx = (unsigned)std::max<int64_t>(1, std::min(want, cap));
   k_draw<<<dim3(gx, a.n_slots, a.n_suggest), 256, 0, st>>>(a);
+  return hipGetLastError();
+}
+
+hipError_t launch_sort_cand(const ScoreArgs &a, int32_t *pos_out, hipStream_t st) {
+  if (a.n_slots <= 0 || a.n_suggest <= 0 || a.n_cand <= 0) return hipSuccess;
+  const unsigned gx = (unsigned)((a.n_cand + kSortMax - 1) / kSortMax);
+  k_sort_cand<<<dim3(gx, a.n_slots, a.n_suggest), 1024, (size_t)kSortMax * 12, st>>>(a, pos_out);
   return hipGetLastError();
 }
 
