@@ -37,7 +37,8 @@ EXPORTS = (
     'tpe_lpdf', 'tpe_score', 'tpe_sample', 'tpe_plan_create', 'tpe_plan_destroy',
     'tpe_plan_num_levels', 'tpe_plan_set_history', 'tpe_plan_fit', 'tpe_plan_get_mixture',
     'tpe_plan_suggest', 'tpe_plan_merge', 'tpe_plan_score_candidates', 'tpe_plan_last_stats',
-    'tpe_plan_profile', 'tpe_plan_profile_read', 'tpe_microbench',
+    'tpe_plan_profile', 'tpe_plan_profile_read', 'tpe_microbench', 'tpe_plan_get_results',
+    'tpe_plan_results_device',
 )
 
 
@@ -135,6 +136,8 @@ def load_library(path: str = LIB_PATH):
             'tpe_plan_profile': (C.c_int, [vp, i32]),
             'tpe_plan_profile_read': (C.c_int, [vp, i32, _D, C.POINTER(i64), _D]),
             'tpe_microbench': (C.c_int, [vp, i32, _D]),
+            'tpe_plan_get_results': (C.c_int, [vp, vp, i32, vp]),
+            'tpe_plan_results_device': (vp, [vp]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -369,19 +372,31 @@ class Plan(object):
         k = k.value
         return w[:k].copy(), mu[:k].copy(), sg[:k].copy()
 
-    def suggest(self, seeds, n_cand, cand_begin=0, level=-1, out=None, stream=None):
+    def suggest(self, seeds, n_cand, cand_begin=0, level=-1, out=None, stream=None, fetch=True):
         """Returns a structured array [n_suggest, n_hp] of RESULT_DTYPE (host)
-        unless ``out`` is a device pointer (int)."""
+        unless ``out`` is a device pointer (int) or ``fetch`` is False (the
+        results stay in the plan: ``results_device_ptr()`` / ``results()``)."""
         e = self.engine
         seeds = np.ascontiguousarray(np.atleast_1d(seeds), dtype=np.uint64)
-        host = out is None
+        host = out is None and fetch
         res = np.empty((seeds.size, self.n_hp), dtype=RESULT_DTYPE) if host else None
         optr = res.ctypes.data if host else out
         with e.lock:
             e.check(e.lib.tpe_plan_suggest(self.p, seeds.ctypes.data_as(C.POINTER(C.c_uint64)),
                                            seeds.size, int(n_cand), int(cand_begin), int(level),
                                            optr, 0 if host else 1, stream))
+        self._last_nsug = seeds.size
         return res
+
+    def results(self):
+        e = self.engine
+        res = np.empty((getattr(self, '_last_nsug', 1), self.n_hp), dtype=RESULT_DTYPE)
+        with e.lock:
+            e.check(e.lib.tpe_plan_get_results(self.p, res.ctypes.data, 0, None))
+        return res
+
+    def results_device_ptr(self):
+        return self.engine.lib.tpe_plan_results_device(self.p)
 
     def merge(self, gathered_ptr, world, level, out=None, stream=None, n_suggest=1):
         e = self.engine

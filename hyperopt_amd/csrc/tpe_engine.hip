@@ -20,6 +20,8 @@ using namespace tpe;
 struct tpe_engine {
   int32_t device = 0;
   hipStream_t stream = nullptr;
+  static constexpr int kAux = 4;
+  hipStream_t aux[kAux] = {};  // concurrent scoring kinds of one level
   std::string err;
   tpe_plan *op = nullptr;  // cached single-hp plan for operator-level calls
 };
@@ -51,6 +53,10 @@ struct tpe_plan {
   uint64_t *d_seeds = nullptr;
   Partial *d_partial = nullptr;
   size_t partial_cap = 0;
+  uint32_t *d_ticket = nullptr;
+  std::vector<uint64_t> h_seeds;  // this call's seeds (inline kernel args when <= 8)
+  bool has_erf = false;
+  hipEvent_t ev_fork = nullptr, ev_join[8] = {};
   double *d_ext = nullptr, *d_lb = nullptr, *d_la = nullptr;
   size_t ext_cap = 0;
   double *d_cand = nullptr;
@@ -104,10 +110,13 @@ void plan_free_buffers(tpe_plan *p) {
   void *bufs[] = {p->d_hps, p->d_cp, p->d_cb, p->d_level_hps, p->d_all_hps, p->d_pprior,
                   p->d_losses, p->d_vals, p->d_active, p->d_below, p->d_mw, p->d_mmu,
                   p->d_msig, p->d_scratch, p->d_info, p->d_coef, p->d_results, p->d_seeds,
-                  p->d_partial, p->d_ext, p->d_lb, p->d_la, p->d_cand, p->d_cpos};
+                  p->d_partial, p->d_ext, p->d_lb, p->d_la, p->d_cand, p->d_cpos,
+                  p->d_ticket};
   for (void *b : bufs) dfree(b);
   if (p->ev0) (void)hipEventDestroy(p->ev0);
   if (p->ev1) (void)hipEventDestroy(p->ev1);
+  if (p->ev_fork) (void)hipEventDestroy(p->ev_fork);
+  for (auto e : p->ev_join) if (e) (void)hipEventDestroy(e);
   for (auto &pr : p->prof) {
     for (auto e : pr.a) (void)hipEventDestroy(e);
     for (auto e : pr.b) (void)hipEventDestroy(e);
@@ -207,6 +216,10 @@ int plan_build(tpe_engine *h, const tpe_space *sp, int64_t max_trials, tpe_plan 
   for (const auto &x : p->hps)
     if (x.family == TPE_CAT) kcap = std::max<int64_t>(kcap, x.upper);
   p->kcap = kcap;
+  for (const auto &x : p->hps) {
+    const int k = score_kind(x);
+    if (k == KIND_ERF_G || k == KIND_ERF_L) p->has_erf = true;
+  }
   const int64_t slots = 2 * (int64_t)p->P;
   CKH(hipSetDevice(h->device));
   CKH(dalloc(&p->d_hps, p->P));
@@ -227,6 +240,8 @@ int plan_build(tpe_engine *h, const tpe_space *sp, int64_t max_trials, tpe_plan 
   CKH(dalloc(&p->d_coef, (size_t)slots * kcap));
   CKH(hipEventCreate(&p->ev0));
   CKH(hipEventCreate(&p->ev1));
+  CKH(hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming));
+  for (auto &e : p->ev_join) CKH(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   std::vector<int32_t> lh;
   for (auto &l : p->levels) lh.insert(lh.end(), l.begin(), l.end());
   std::vector<int32_t> all(p->P);
@@ -250,10 +265,14 @@ int ensure_suggest_state(tpe_engine *h, tpe_plan *p, int64_t n_sug, size_t parti
   if (n_sug > p->s_cap) {
     dfree(p->d_results);
     dfree(p->d_seeds);
+    dfree(p->d_ticket);
     p->d_results = nullptr;
     p->d_seeds = nullptr;
+    p->d_ticket = nullptr;
     CKH(dalloc(&p->d_results, (size_t)n_sug * p->P));
     CKH(dalloc(&p->d_seeds, n_sug));
+    CKH(dalloc(&p->d_ticket, (size_t)n_sug * p->P));
+    CKH(hipMemset(p->d_ticket, 0, (size_t)n_sug * p->P * sizeof(uint32_t)));
     p->s_cap = n_sug;
   }
   if (partials > p->partial_cap) {
@@ -319,14 +338,9 @@ double group_pairs(tpe_plan *p, int kind, int32_t n_slots, int64_t cn, int64_t n
   return (double)cn * (double)n_sug;  // x (K_b + K_a) applied at read time
 }
 
-// One (level, kind) group: draw candidates (unless external), score, reduce.
-// Candidates are processed in chunks so the buffer stays <= 512 MB.
-int run_group(tpe_engine *h, tpe_plan *p, int32_t kind, const int32_t *level_hps_dev,
-              int32_t n_slots, int64_t n_sug, int64_t n_cand, int64_t cand_begin,
-              const double *ext, double *lb, double *la, int32_t force, hipStream_t st) {
+ScoreArgs base_args(tpe_plan *p, int64_t n_sug) {
   ScoreArgs a{};
   a.hps = p->d_hps;
-  a.level_hps = level_hps_dev;
   a.cond_parent = p->d_cp;
   a.cond_branch = p->d_cb;
   a.info = p->d_info;
@@ -335,62 +349,117 @@ int run_group(tpe_engine *h, tpe_plan *p, int32_t kind, const int32_t *level_hps
   a.mmu = p->d_mmu;
   a.msig = p->d_msig;
   a.seeds = p->d_seeds;
-  a.out_lb = lb;
-  a.out_la = la;
   a.results = p->d_results;
+  a.partial = p->d_partial;
+  a.ticket = p->d_ticket;
   a.kcap = p->kcap;
   a.n_hp = p->P;
-  a.n_slots = n_slots;
   a.n_suggest = (int32_t)n_sug;
-  a.force_active = force;
+  return a;
+}
+
+int score_launch(tpe_engine *h, tpe_plan *p, ScoreArgs a, int32_t kind, int32_t grid_x,
+                 int64_t cn, hipStream_t sg, bool record) {
+  tpe_plan::Prof *pr = nullptr;
+  if (record && p->prof_cap > 0) {
+    pr = &p->prof[kind];
+    if (pr->n >= p->prof_cap) pr = nullptr;  // ring full: stop recording
+  }
+  if (pr) CKH(hipEventRecord(pr->a[pr->n], sg));
+  CKH(launch_score(a, kind, grid_x, sg));
+  if (pr) {
+    CKH(hipEventRecord(pr->b[pr->n], sg));
+    pr->pairs[pr->n] = group_pairs(p, kind, a.n_slots, cn, a.n_suggest);
+    pr->n++;
+  }
+  return TPE_OK;
+}
+
+// One level of conditional hps: one draw(+sort) launch for all of its hps,
+// then one fused score+argmax launch per lpdf kind, the kinds running
+// concurrently on the engine's auxiliary streams.  Candidates are processed
+// in chunks so the buffer stays <= 512 MB.
+int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_cand,
+              int64_t cand_begin, hipStream_t st) {
+  const auto &groups = p->groups[level];
+  const int32_t n_level = (int32_t)p->levels[level].size();
+  const int32_t *lvl = p->d_level_hps + p->level_off[level];
   const int64_t budget = (int64_t)64 << 20;  // doubles
-  const int64_t chunk = ext ? std::max<int64_t>(n_cand, 1)
-                            : std::max<int64_t>(1, std::min<int64_t>(std::max<int64_t>(n_cand, 1),
-                                                   budget / std::max<int64_t>(1, n_sug * n_slots)));
+  const int64_t chunk = std::max<int64_t>(
+      1, std::min<int64_t>(std::max<int64_t>(n_cand, 1),
+                           budget / std::max<int64_t>(1, n_sug * n_level)));
   int64_t c0 = 0;
   do {
     const int64_t cn = std::min(chunk, n_cand - c0);
-    int32_t ks, tiles, grid_x;
-    choose_geometry(cn, n_slots, n_sug, kind, ks, tiles, grid_x);
-    int rc = ensure_suggest_state(h, p, n_sug, (size_t)n_sug * n_slots * grid_x);
+    std::vector<int32_t> ks(groups.size()), tiles(groups.size()), gx(groups.size());
+    int32_t pstride = 1;
+    for (size_t g = 0; g < groups.size(); ++g) {
+      choose_geometry(cn, groups[g].count, n_sug, groups[g].kind, ks[g], tiles[g], gx[g]);
+      pstride = std::max(pstride, gx[g]);
+    }
+    int rc = ensure_suggest_state(h, p, n_sug, (size_t)n_sug * p->P * pstride);
     if (rc) return rc;
-    a.partial = p->d_partial;
-    a.results = p->d_results;
-    a.seeds = p->d_seeds;
+    rc = ensure_cand(h, p, (size_t)std::max<int64_t>(1, n_sug * n_level * cn));
+    if (rc) return rc;
+    ScoreArgs a = base_args(p, n_sug);
+    a.cand = p->d_cand;
+    a.cand_sstride = (int64_t)n_level * cn;
     a.n_cand = cn;
     a.cand_begin = cand_begin + c0;
-    a.ks = ks;
-    a.tiles = tiles;
-    a.cand_pos = nullptr;
-    if (ext) {
-      a.cand = ext;
-    } else {
-      rc = ensure_cand(h, p, (size_t)std::max<int64_t>(1, n_sug * n_slots * cn));
+    a.pstride = pstride;
+    a.accumulate = c0 > 0 ? 1 : 0;
+    a.level_hps = lvl;
+    a.n_slots = n_level;
+    for (int i = 0; i < kInlineSeeds && i < n_sug; ++i) a.seed_inline[i] = p->h_seeds[i];
+    a.n_inline_seeds = (int32_t)std::min<int64_t>(n_sug, kInlineSeeds);
+    CKH(launch_draw(a, st));
+    if (p->has_erf) CKH(launch_bucket(a, p->d_cpos, st));
+    const bool fork = groups.size() > 1;
+    if (fork) CKH(hipEventRecord(p->ev_fork, st));
+    for (size_t g = 0; g < groups.size(); ++g) {
+      hipStream_t sg = (g == 0 || g > (size_t)tpe_engine::kAux) ? st : h->aux[g - 1];
+      if (sg != st) CKH(hipStreamWaitEvent(sg, p->ev_fork, 0));
+      ScoreArgs b = a;
+      const int32_t rel = groups[g].off - p->level_off[level];
+      b.level_hps = lvl + rel;
+      b.n_slots = groups[g].count;
+      b.cand_slot0 = rel;
+      b.cand_pos = (groups[g].kind == KIND_ERF_G || groups[g].kind == KIND_ERF_L) ? p->d_cpos
+                                                                                     : nullptr;
+      b.ks = ks[g];
+      b.tiles = tiles[g];
+      rc = score_launch(h, p, b, groups[g].kind, gx[g], cn, sg, true);
       if (rc) return rc;
-      a.cand = p->d_cand;
-      CKH(launch_draw(a, st));
-      if (kind == KIND_ERF_G || kind == KIND_ERF_L) {  // wave-coherent erf skipping
-        CKH(launch_sort_cand(a, p->d_cpos, st));
-        a.cand_pos = p->d_cpos;
-      }
+      if (sg != st) CKH(hipEventRecord(p->ev_join[g % 8], sg));
     }
-    tpe_plan::Prof *pr = nullptr;
-    if (p->prof_cap > 0 && !ext) {
-      pr = &p->prof[kind];
-      if (pr->n >= p->prof_cap) pr = nullptr;  // ring full: stop recording
-    }
-    if (pr) CKH(hipEventRecord(pr->a[pr->n], st));
-    CKH(launch_score(a, kind, grid_x, st));
-    if (pr) {
-      CKH(hipEventRecord(pr->b[pr->n], st));
-      pr->pairs[pr->n] = group_pairs(p, kind, n_slots, cn, n_sug);
-      pr->n++;
-    }
-    CKH(launch_reduce(level_hps_dev, n_slots, (int32_t)n_sug, p->P, grid_x, c0 > 0 ? 1 : 0,
-                      p->d_partial, p->d_results, st));
+    for (size_t g = 1; g < groups.size() && g <= (size_t)tpe_engine::kAux; ++g)
+      CKH(hipStreamWaitEvent(st, p->ev_join[g % 8], 0));
     c0 += cn;
   } while (c0 < n_cand);
   return TPE_OK;
+}
+
+// Externally supplied candidates of one hp (parity / operator path).
+int run_external(tpe_engine *h, tpe_plan *p, int32_t hp, const double *ext, int64_t n,
+                 double *lb, double *la, hipStream_t st) {
+  const int kind = score_kind(p->hps[hp]);
+  int32_t ks, tiles, gx;
+  choose_geometry(n, 1, 1, kind, ks, tiles, gx);
+  int rc = ensure_suggest_state(h, p, 1, (size_t)p->P * gx);
+  if (rc) return rc;
+  ScoreArgs a = base_args(p, 1);
+  a.cand = ext;
+  a.cand_sstride = n;
+  a.n_cand = n;
+  a.pstride = gx;
+  a.level_hps = p->d_all_hps + hp;
+  a.n_slots = 1;
+  a.out_lb = lb;
+  a.out_la = la;
+  a.force_active = 1;
+  a.ks = ks;
+  a.tiles = tiles;
+  return score_launch(h, p, a, kind, gx, n, st, false);
 }
 
 int copy_results(tpe_engine *h, tpe_plan *p, int64_t n_sug, tpe_result *out, int32_t on_dev,
@@ -488,6 +557,11 @@ int tpe_create(int32_t device, tpe_handle_t *out) {
     delete h;
     return TPE_E_HIP;
   }
+  for (auto &a : h->aux)
+    if (hipStreamCreateWithFlags(&a, hipStreamNonBlocking) != hipSuccess) {
+      tpe_destroy(h);
+      return TPE_E_HIP;
+    }
   *out = h;
   return TPE_OK;
 }
@@ -497,6 +571,7 @@ int tpe_destroy(tpe_handle_t h) {
   (void)hipSetDevice(h->device);
   if (h->op) { plan_free_buffers(h->op); delete h->op; }
   if (h->stream) (void)hipStreamDestroy(h->stream);
+  for (auto a : h->aux) if (a) (void)hipStreamDestroy(a);
   delete h;
   return TPE_OK;
 }
@@ -547,8 +622,10 @@ static int fit_one(tpe_handle_t h, int32_t family, const double *obs, int64_t n,
     CKH(hipMemsetAsync(p->d_active, 1, n, h->stream));
     CKH(hipMemsetAsync(p->d_below, 1, n, h->stream));
   }
-  CKH(launch_fit(p->d_hps, 1, p->d_vals, p->d_active, p->d_below, n, prior_weight, lf, p->d_pprior,
-                 p->d_mw, p->d_mmu, p->d_msig, p->d_info, p->kcap, p->d_scratch, h->stream));
+  if (n > 0) CKH(hipMemsetAsync(p->d_losses, 0, n * 8, h->stream));
+  CKH(launch_fit(p->d_hps, 1, p->d_vals, p->d_active, p->d_losses, n, (int32_t)n, prior_weight,
+                 lf, p->d_pprior, p->d_mw, p->d_mmu, p->d_msig, p->d_info, p->d_coef, p->kcap,
+                 p->d_scratch, p->d_scratch, h->stream));
   *pout = p;
   return TPE_OK;
 }
@@ -633,8 +710,8 @@ int tpe_score(tpe_handle_t h, int32_t family, const double *x, int64_t n, const 
   rc = ensure_ext(h, p, n);
   if (rc) return rc;
   CKH(hipMemcpyAsync(p->d_ext, x, n * 8, hipMemcpyHostToDevice, h->stream));
-  rc = run_group(h, p, score_kind(p->hps[0]), p->d_all_hps, 1, 1, n, 0, p->d_ext,
-                 llik_b ? p->d_lb : nullptr, llik_a ? p->d_la : nullptr, 1, h->stream);
+  rc = run_external(h, p, 0, p->d_ext, n, llik_b ? p->d_lb : nullptr,
+                    llik_a ? p->d_la : nullptr, h->stream);
   if (rc) return rc;
   tpe_result r;
   CKH(hipMemcpyAsync(&r, p->d_results, sizeof(r), hipMemcpyDeviceToHost, h->stream));
@@ -742,11 +819,9 @@ int tpe_plan_fit(tpe_plan_t p, double gamma, int32_t gamma_cap, double prior_wei
   hipStream_t st = pick_stream(h, stream);
   const double nbf = std::ceil(gamma * std::sqrt((double)p->n));
   const int32_t nb = (int32_t)std::max(0.0, std::min<double>(nbf, gamma_cap));
-  if (p->n > 0) CKH(launch_split(p->d_losses, p->n, nb, p->d_below, st));
-  CKH(launch_fit(p->d_hps, p->P, p->d_vals, p->d_active, p->d_below, p->n, prior_weight, lf,
-                 p->d_pprior, p->d_mw, p->d_mmu, p->d_msig, p->d_info, p->kcap, p->d_scratch, st));
-  CKH(launch_prep(p->d_hps, p->P, p->d_mw, p->d_mmu, p->d_msig, p->d_info, p->d_coef, p->kcap,
-                  p->d_scratch, st));
+  CKH(launch_fit(p->d_hps, p->P, p->d_vals, p->d_active, p->d_losses, p->n, nb, prior_weight, lf,
+                 p->d_pprior, p->d_mw, p->d_mmu, p->d_msig, p->d_info, p->d_coef, p->kcap,
+                 p->d_scratch, p->d_scratch, st));
   return TPE_OK;
 }
 
@@ -779,22 +854,33 @@ int tpe_plan_suggest(tpe_plan_t p, const uint64_t *seeds, int64_t n_sug, int64_t
   hipStream_t st = pick_stream(h, stream);
   int rc = ensure_suggest_state(h, p, n_sug, 1);
   if (rc) return rc;
-  CKH(hipMemcpyAsync(p->d_seeds, seeds, n_sug * 8, hipMemcpyHostToDevice, st));
+  p->h_seeds.assign(seeds, seeds + n_sug);
+  if (n_sug > kInlineSeeds)
+    CKH(hipMemcpyAsync(p->d_seeds, seeds, n_sug * 8, hipMemcpyHostToDevice, st));
   CKH(hipEventRecord(p->ev0, st));
   const int l0 = level < 0 ? 0 : level;
   const int l1 = level < 0 ? (int)p->levels.size() : level + 1;
-  for (int l = l0; l < l1; ++l)
-    for (const auto &g : p->groups[l]) {
-      rc = run_group(h, p, g.kind, p->d_level_hps + g.off, g.count, n_sug, n_cand, cand_begin,
-                     nullptr, nullptr, nullptr, 0, st);
-      if (rc) return rc;
-    }
+  for (int l = l0; l < l1; ++l) {
+    rc = run_level(h, p, l, n_sug, n_cand, cand_begin, st);
+    if (rc) return rc;
+  }
   CKH(hipEventRecord(p->ev1, st));
   p->timed = true;
   p->last_ncand = n_cand;
   p->last_nsug = n_sug;
   p->last_level = level;
   return copy_results(h, p, n_sug, out, out_on_device, st);
+}
+
+int tpe_plan_get_results(tpe_plan_t p, tpe_result *out, int32_t out_on_device, void *stream) {
+  if (!p || !out) return TPE_E_INVALID;
+  tpe_engine *h = p->eng;
+  CKH(hipSetDevice(h->device));
+  return copy_results(h, p, p->last_nsug, out, out_on_device, pick_stream(h, stream));
+}
+
+const tpe_result *tpe_plan_results_device(tpe_plan_t p) {
+  return p ? reinterpret_cast<const tpe_result *>(p->d_results) : nullptr;
 }
 
 int tpe_plan_merge(tpe_plan_t p, const tpe_result *gathered, int32_t world, int32_t level,
@@ -831,8 +917,8 @@ int tpe_plan_score_candidates(tpe_plan_t p, int32_t hp, const double *x, int64_t
   int rc = ensure_ext(h, p, n);
   if (rc) return rc;
   CKH(hipMemcpyAsync(p->d_ext, x, n * 8, hipMemcpyHostToDevice, st));
-  rc = run_group(h, p, score_kind(H), p->d_all_hps + hp, 1, 1, n, 0, p->d_ext,
-                 llik_b ? p->d_lb : nullptr, llik_a ? p->d_la : nullptr, 1, st);
+  rc = run_external(h, p, hp, p->d_ext, n, llik_b ? p->d_lb : nullptr,
+                    llik_a ? p->d_la : nullptr, st);
   if (rc) return rc;
   tpe_result r;
   CKH(hipMemcpyAsync(&r, p->d_results + hp, sizeof(r), hipMemcpyDeviceToHost, st));

@@ -49,7 +49,11 @@ struct Partial {  // == tpe_result layout
 };
 static_assert(sizeof(Partial) == sizeof(tpe_result), "layout");
 
+constexpr int kInlineSeeds = 8;  // suggestion seeds passed by value
+
 struct ScoreArgs {
+  uint64_t seed_inline[kInlineSeeds];
+  int32_t n_inline_seeds;
   const tpe_hp *hps;
   const int32_t *level_hps;  // hp ids of this launch (blockIdx.y)
   const int32_t *cond_parent;
@@ -62,33 +66,39 @@ struct ScoreArgs {
   const int32_t *cand_pos;   // optional: original position of each (sorted) candidate
   double *out_lb, *out_la;   // optional per-candidate lliks (ext only)
   Partial *results;          // [S][P]
-  Partial *partial;          // [S][n_slots][grid.x]
+  Partial *partial;          // [S][P][pstride] block argmax records
+  uint32_t *ticket;          // [S][P] arrival counters (zero between launches)
   int64_t kcap;
   int64_t n_cand;
   int64_t cand_begin;
+  int64_t cand_sstride;      // candidate elements per suggestion in `cand`
+  int32_t cand_slot0;        // slot of blockIdx.y == 0 within the candidate buffer
+  int32_t pstride;           // partial records per (s, hp)
   int32_t n_hp;
   int32_t n_slots;
-  int32_t ks;                // component split across the 4 waves (1,2,4)
+  int32_t ks;                // waves of a 16-wave block sharing 64 candidates
   int32_t tiles;             // candidate tiles per (s, hp)
   int32_t n_suggest;         // grid.z
   int32_t force_active;      // ignore conditions (operator-level scoring)
+  int32_t accumulate;        // merge with results of an earlier candidate chunk
 };
 
 // ---- launch wrappers (tpe_kernels.hip) ----
 hipError_t launch_split(const double *losses, int64_t n, int32_t n_below,
                         uint8_t *below, hipStream_t st);
 hipError_t launch_fit(const tpe_hp *hps, int32_t n_hp, const double *vals,
-                      const uint8_t *active, const uint8_t *below, int64_t n,
-                      double prior_weight, int32_t lf, const double *pprior,
-                      double *mw, double *mmu, double *msig, MixInfo *info,
-                      int64_t kcap, double *scratch, hipStream_t st);
+                      const uint8_t *active, const double *losses, int64_t n,
+                      int32_t n_below, double prior_weight, int32_t lf,
+                      const double *pprior, double *mw, double *mmu, double *msig,
+                      MixInfo *info, Coef *coef, int64_t kcap, double *scratch,
+                      double *scratch2, hipStream_t st);
 hipError_t launch_prep(const tpe_hp *hps, int32_t n_hp, const double *mw,
                        const double *mmu, const double *msig, MixInfo *info,
                        Coef *coef, int64_t kcap, double *scratch,
                        hipStream_t st);
 hipError_t launch_score(const ScoreArgs &a, int32_t kind, int32_t grid_x, hipStream_t st);
 hipError_t launch_draw(const ScoreArgs &a, hipStream_t st);
-hipError_t launch_sort_cand(const ScoreArgs &a, int32_t *pos_out, hipStream_t st);
+hipError_t launch_bucket(const ScoreArgs &a, int32_t *pos_out, hipStream_t st);
 hipError_t launch_reduce(const int32_t *level_hps, int32_t n_slots,
                          int32_t n_suggest, int32_t n_hp, int32_t grid_x,
                          int32_t accumulate, const Partial *partial,

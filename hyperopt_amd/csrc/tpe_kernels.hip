@@ -308,15 +308,56 @@ struct FitSmem {
   NpSumSmem np;
 };
 
+__device__ void prep_slot(const tpe_hp &H, int64_t slot, const double *w, const double *mu,
+                          const double *sg, MixInfo *info, Coef *coef, int64_t kcap,
+                          double *scratch, NpSumSmem &np);
+
+// The n_below-th smallest loss key (value, position) in numpy argsort order
+// (NaN last, ties by position): one wave, n_below <= 25 rounds of a wave-wide
+// argmin over the keys above the previous winner -- no block barriers.
+// below(j) <=> key(j) <= threshold.  n_below == 0 -> position -1 (none).
+__device__ void split_threshold(const double *__restrict__ losses, int64_t n, int32_t n_below,
+                                double &tv, int64_t &ti) {
+  double pv = -INFINITY;
+  int64_t pi = -1;
+  const int lane = threadIdx.x & 63;
+  for (int r = 0; r < n_below && r < n; ++r) {
+    double bv = NAN;
+    int64_t bi = -1;
+    for (int64_t j = lane; j < n; j += 64) {
+      const double v = losses[j];
+      if (pi >= 0 && !key_less(pv, pi, v, j)) continue;
+      if (bi < 0 || key_less(v, j, bv, bi)) { bv = v; bi = j; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double ov = __shfl_xor(bv, o, 64);
+      const int64_t oi = __shfl_xor(bi, o, 64);
+      if (oi >= 0 && (bi < 0 || key_less(ov, oi, bv, bi))) { bv = ov; bi = oi; }
+    }
+    pv = bv;
+    pi = bi;
+  }
+  tv = pv;
+  ti = pi;
+}
+
+// Split + Parzen fit (or categorical posterior) + lpdf constants of one
+// (hp, side) slot, one 1024-thread block each: tpe.py:613-641, 381-475,
+// 573-607, 104-166, 259-301 in a single launch.
 __global__ __launch_bounds__(1024) void k_fit(
     const tpe_hp *__restrict__ hps, const double *__restrict__ vals,
-    const uint8_t *__restrict__ active, const uint8_t *__restrict__ below,
-    int64_t n, double prior_weight, int32_t lf, const double *__restrict__ pprior,
+    const uint8_t *__restrict__ active, const double *__restrict__ losses,
+    int64_t n, int32_t n_below, double prior_weight, int32_t lf,
+    const double *__restrict__ pprior,
     double *__restrict__ mw, double *__restrict__ mmu, double *__restrict__ msig,
-    MixInfo *__restrict__ info, int64_t kcap, double *__restrict__ scratch) {
+    MixInfo *__restrict__ info, Coef *__restrict__ coef, int64_t kcap,
+    double *__restrict__ scratch, double *__restrict__ scratch2) {
 #pragma clang fp contract(off)
   extern __shared__ __attribute__((aligned(16))) double dyn_lds[];
   __shared__ FitSmem sm;
+  __shared__ double thr_v;
+  __shared__ int64_t thr_i;
   const int hp = blockIdx.x, side = blockIdx.y;  // side 0 = below ("good")
   const int64_t slot = 2 * (int64_t)hp + side;
   const tpe_hp H = hps[hp];
@@ -326,15 +367,28 @@ __global__ __launch_bounds__(1024) void k_fit(
   double *ob = scratch + slot * kcap;  // observations in tid order
   const double *row = vals + (int64_t)hp * n;
   const uint8_t *arow = active + (int64_t)hp * n;
-  const uint8_t want = side == 0 ? 1 : 0;
+  // ---- good/bad split: threshold key of the n_below best losses
+  if (threadIdx.x < 64) {
+    double tv;
+    int64_t ti;
+    split_threshold(losses, n, n_below, tv, ti);
+    if (threadIdx.x == 0) { thr_v = tv; thr_i = ti; }
+  }
+  __syncthreads();
+  const double tv = thr_v;
+  const int64_t ti = thr_i;
 
   // ---- gather this side's observations, keeping tid order (tpe.py:629-636)
   int m = 0;
   for (int64_t c0 = 0; c0 < n; c0 += blockDim.x) {
     const int64_t j = c0 + threadIdx.x;
-    const int f = (j < n && arow[j] && below[j] == want) ? 1 : 0;
+    bool f = j < n && arow[j];
+    if (f) {
+      const bool good = ti >= 0 && !key_less(tv, ti, losses[j], j);   // key(j) <= thr
+      f = good == (side == 0);
+    }
     int tot;
-    const int pos = block_excl_scan(f, sm.wsum, tot);
+    const int pos = block_excl_scan(f ? 1 : 0, sm.wsum, tot);
     if (f) ob[m + pos] = obs_transform(row[j], H.obs_transform, H.low);
     m += tot;
   }
@@ -387,6 +441,8 @@ __global__ __launch_bounds__(1024) void k_fit(
       sg[c] = 0.0;
     }
     if (threadIdx.x == 0) { info[slot].K = upper; info[slot].kind = 2; }
+    __syncthreads();
+    prep_slot(H, slot, w, mu, sg, info, coef, kcap, scratch2, sm.np);
     return;
   }
 
@@ -470,6 +526,8 @@ __global__ __launch_bounds__(1024) void k_fit(
   const double tot = block_np_sum(w, K, sm.np);
   for (int k = threadIdx.x; k < K; k += blockDim.x) w[k] = w[k] / tot;
   if (threadIdx.x == 0) { info[slot].K = K; info[slot].kind = 0; }
+  __syncthreads();
+  prep_slot(H, slot, w, mu, sg, info, coef, kcap, scratch2, sm.np);
 }
 
 // ------------------------------------------------------------------------
@@ -482,20 +540,12 @@ __device__ __forceinline__ double normal_cdf(double x, double mu, double sigma) 
   return 0.5 * (1.0 + erf(z));
 }
 
-__global__ __launch_bounds__(256) void k_prep(
-    const tpe_hp *__restrict__ hps, const double *__restrict__ mw,
-    const double *__restrict__ mmu, const double *__restrict__ msig,
-    MixInfo *__restrict__ info, Coef *__restrict__ coef, int64_t kcap,
-    double *__restrict__ scratch) {
+// Per-component lpdf constants + truncation mass of one slot (block-wide).
+__device__ void prep_slot(const tpe_hp &H, int64_t slot, const double *w, const double *mu,
+                          const double *sg, MixInfo *info, Coef *coef, int64_t kcap,
+                          double *scratch, NpSumSmem &np) {
 #pragma clang fp contract(off)
-  __shared__ NpSumSmem np;
-  const int hp = blockIdx.x, side = blockIdx.y;
-  const int64_t slot = 2 * (int64_t)hp + side;
-  const tpe_hp H = hps[hp];
   const int K = info[slot].K;
-  const double *w = mw + slot * kcap;
-  const double *mu = mmu + slot * kcap;
-  const double *sg = msig + slot * kcap;
   Coef *cf = coef + slot * kcap;
   double *tmp = scratch + slot * kcap;
   const double wsum = block_np_sum(w, K, np);
@@ -548,6 +598,20 @@ __global__ __launch_bounds__(256) void k_prep(
     info[slot].log_pacc = log(pacc);
     info[slot].wsum = wsum;
   }
+}
+
+// Constants of explicitly given mixtures (operator-level tpe_score/lpdf).
+__global__ __launch_bounds__(256) void k_prep(
+    const tpe_hp *__restrict__ hps, const double *__restrict__ mw,
+    const double *__restrict__ mmu, const double *__restrict__ msig,
+    MixInfo *__restrict__ info, Coef *__restrict__ coef, int64_t kcap,
+    double *__restrict__ scratch) {
+  __shared__ NpSumSmem np;
+  const int hp = blockIdx.x, side = blockIdx.y;
+  const int64_t slot = 2 * (int64_t)hp + side;
+  const tpe_hp H = hps[hp];
+  prep_slot(H, slot, mw + slot * kcap, mmu + slot * kcap, msig + slot * kcap, info, coef, kcap,
+            scratch, np);
 }
 
 // ------------------------------------------------------------------------
@@ -718,9 +782,14 @@ __device__ __forceinline__ bool hp_active(const tpe_hp &H, const Partial *res,
   return false;
 }
 
-// Candidate draws of one (level, kind) group: grid = (blocks, hps, suggestions).
-// Counter = (global candidate index, hp id, iteration), key = suggestion seed,
-// so the candidate set does not depend on how [0, n_cand) is sharded.
+__device__ __forceinline__ uint64_t suggestion_seed(const ScoreArgs &A, int s) {
+  return s < kInlineSeeds && A.n_inline_seeds > s ? A.seed_inline[s] : A.seeds[s];
+}
+
+// Candidate draws of one level (all its hps): grid = (blocks, hps of the
+// level, suggestions), one candidate per thread per step.  Counter = (global
+// candidate index, hp id, iteration), key = suggestion seed, so the
+// candidate set does not depend on how [0, n_cand) is chunked or sharded.
 __global__ __launch_bounds__(256) void k_draw(ScoreArgs A) {
   const int slot = blockIdx.y, s = blockIdx.z;
   const int hp = A.level_hps[slot];
@@ -729,38 +798,77 @@ __global__ __launch_bounds__(256) void k_draw(ScoreArgs A) {
   const int64_t sb = 2 * (int64_t)hp;
   const MixInfo ib = A.info[sb];
   const double *bw = A.mw + sb * A.kcap, *bmu = A.mmu + sb * A.kcap, *bsg = A.msig + sb * A.kcap;
-  const uint64_t seed = A.seeds[s];
-  double *out = const_cast<double *>(A.cand) + ((int64_t)s * A.n_slots + slot) * A.n_cand;
+  const uint64_t seed = suggestion_seed(A, s);
+  double *out = const_cast<double *>(A.cand) + (int64_t)s * A.cand_sstride + (int64_t)slot * A.n_cand;
   for (int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; li < A.n_cand;
        li += (int64_t)gridDim.x * blockDim.x)
     out[li] = draw_one(H, ib, bw, bmu, bsg, seed, (uint64_t)(A.cand_begin + li), (uint32_t)hp);
 }
 
-// Sort each 8192-candidate chunk of every (suggestion, hp) by value, keeping
-// the original position: a wave then holds 64 neighbouring candidates, so a
-// mixture component far from all of them (erf saturated, exp underflowed)
-// is skipped by the whole wave.  Scores and argmax tie-breaks still use the
-// original global candidate index.
-__global__ __launch_bounds__(1024) void k_sort_cand(ScoreArgs A, int32_t *__restrict__ pos_out) {
+// Bucket each 8192-candidate chunk of the erf-kind hps by value (counting
+// sort into 256 equal-width buckets of the chunk's range, in the coordinate
+// the erf argument is linear in), keeping each candidate's original
+// position.  A wave then holds neighbouring candidates and a mixture
+// component far from all of them (both erf saturated) is skipped by the
+// whole wave.  Order inside a bucket is irrelevant: every candidate is
+// scored on its own and the argmax tie-break uses the original index.
+constexpr int kBuckets = 256;
+__global__ __launch_bounds__(1024) void k_bucket(ScoreArgs A, int32_t *__restrict__ pos_out) {
   extern __shared__ __attribute__((aligned(16))) double dyn_lds[];
+  __shared__ int hist[kBuckets];
+  __shared__ double red_lo[16], red_hi[16];
   const int slot = blockIdx.y, s = blockIdx.z;
   const int hp = A.level_hps[slot];
-  if (!A.force_active &&
-      !hp_active(A.hps[hp], A.results + (int64_t)s * A.n_hp, A.cond_parent, A.cond_branch))
-    return;
+  const tpe_hp H = A.hps[hp];
+  const int kind = score_kind(H);
+  if (kind != KIND_ERF_G && kind != KIND_ERF_L) return;
+  if (!hp_active(H, A.results + (int64_t)s * A.n_hp, A.cond_parent, A.cond_branch)) return;
   const int64_t base = (int64_t)blockIdx.x * kSortMax;
   if (base >= A.n_cand) return;
   const int n = (int)min<int64_t>(kSortMax, A.n_cand - base);
-  double *cand = const_cast<double *>(A.cand) + ((int64_t)s * A.n_slots + slot) * A.n_cand + base;
-  int32_t *po = pos_out + ((int64_t)s * A.n_slots + slot) * A.n_cand + base;
-  double *key = dyn_lds;
-  int *pos = reinterpret_cast<int *>(dyn_lds + kSortMax);
-  for (int i = threadIdx.x; i < n; i += blockDim.x) { key[i] = cand[i]; pos[i] = i; }
-  __syncthreads();
-  block_bitonic_sort(key, pos, n, pow2_at_least(n));
+  const int64_t off = (int64_t)s * A.cand_sstride + (int64_t)slot * A.n_cand + base;
+  double *cand = const_cast<double *>(A.cand) + off;
+  double *xs = dyn_lds;                                        // [8192] values
+  unsigned char *bk = reinterpret_cast<unsigned char *>(dyn_lds + kSortMax);  // [8192]
+  const bool lg = kind == KIND_ERF_L;
+  double lo = INFINITY, hi = -INFINITY;
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    cand[i] = key[i];
-    po[i] = (int32_t)(base + pos[i]);
+    const double x = cand[i];
+    xs[i] = x;
+    const double t = lg ? log(fmax(x, 1e-300)) : x;
+    if (t == t && fabs(t) < INFINITY) { lo = fmin(lo, t); hi = fmax(hi, t); }
+  }
+  for (int b = threadIdx.x; b < kBuckets; b += blockDim.x) hist[b] = 0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = fmin(lo, __shfl_xor(lo, o, 64));
+    hi = fmax(hi, __shfl_xor(hi, o, 64));
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) { red_lo[wid] = lo; red_hi[wid] = hi; }
+  __syncthreads();
+  lo = INFINITY; hi = -INFINITY;
+  for (int w = 0; w < (int)(blockDim.x >> 6); ++w) { lo = fmin(lo, red_lo[w]); hi = fmax(hi, red_hi[w]); }
+  const double scale = hi > lo ? (double)kBuckets / (hi - lo) : 0.0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const double x = xs[i];
+    const double t = lg ? log(fmax(x, 1e-300)) : x;
+    int b = kBuckets - 1;
+    if (t == t && fabs(t) < INFINITY) b = min(kBuckets - 1, max(0, (int)((t - lo) * scale)));
+    bk[i] = (unsigned char)b;
+    atomicAdd(&hist[b], 1);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int b = 0; b < kBuckets; ++b) { const int c = hist[b]; hist[b] = acc; acc += c; }
+  }
+  __syncthreads();
+  int32_t *po = pos_out + off;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int p = atomicAdd(&hist[bk[i]], 1);
+    cand[p] = xs[i];
+    po[p] = (int32_t)(base + i);
   }
 }
 
@@ -784,21 +892,22 @@ __global__ __launch_bounds__(1024) void k_score(ScoreArgs A, const Coef *__restr
   const int slot = blockIdx.y, s = blockIdx.z;
   const int hp = A.level_hps[slot];
   const tpe_hp H = A.hps[hp];
-  Partial *pout = A.partial + ((int64_t)s * A.n_slots + slot) * gridDim.x + blockIdx.x;
+  Partial *pbase = A.partial + ((int64_t)s * A.n_hp + hp) * A.pstride;
+  Partial *pout = pbase + blockIdx.x;
 
   const bool act = A.force_active || hp_active(H, A.results + (int64_t)s * A.n_hp,
                                                   A.cond_parent, A.cond_branch);
-  if (!act) {
-    if (threadIdx.x == 0) *pout = Partial{NAN, NAN, -1, 0, 0};
+  if (!act) {   // every block writes the same "inactive" record
+    if (threadIdx.x == 0) A.results[(int64_t)s * A.n_hp + hp] = Partial{NAN, NAN, -1, 0, 0};
     return;
   }
   const int64_t sb = 2 * (int64_t)hp, sa = sb + 1;
   const MixInfo ib = A.info[sb], ia = A.info[sa];
   const Coef *__restrict__ cb = coef + sb * A.kcap;
   const Coef *__restrict__ ca = coef + sa * A.kcap;
-  const double *__restrict__ cand = cand_all + ((int64_t)s * A.n_slots + slot) * A.n_cand;
-  const int32_t *__restrict__ cpos =
-      A.cand_pos ? A.cand_pos + ((int64_t)s * A.n_slots + slot) * A.n_cand : nullptr;
+  const int64_t coff = (int64_t)s * A.cand_sstride + (int64_t)(A.cand_slot0 + slot) * A.n_cand;
+  const double *__restrict__ cand = cand_all + coff;
+  const int32_t *__restrict__ cpos = A.cand_pos ? A.cand_pos + coff : nullptr;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int ks = A.ks, groups = kScoreWaves / ks;
   const int grp = wave / ks, kp = wave % ks;
@@ -885,10 +994,38 @@ __global__ __launch_bounds__(1024) void k_score(ScoreArgs A, const Coef *__restr
   wave_best(best_s, best_v, best_i);
   if (lane == 0) { bs[wave] = best_s; bv[wave] = best_v; bi[wave] = best_i; }
   __syncthreads();
+  __shared__ int last;
   if (threadIdx.x == 0) {
     for (int w = 1; w < kScoreWaves; ++w)
       if (better(bs[w], bi[w], best_s, best_i)) { best_s = bs[w]; best_v = bv[w]; best_i = bi[w]; }
     *pout = Partial{best_s, best_v, best_i, 1, 0};
+    // publish the block record, then take an arrival ticket (agent-scope
+    // release / acquire, cdna_hip_programming.md Guideline 16 counter form)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t *tk = A.ticket + (int64_t)s * A.n_hp + hp;
+    const uint32_t t = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = (t == gridDim.x - 1) ? 1 : 0;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  if (!last || wave != 0) return;
+  // the last-arriving block reduces every block's record (k_reduce fused)
+  double fs = NAN, fv = NAN;
+  int64_t fi = -1;
+  for (int i = lane; i < (int)gridDim.x; i += 64) {
+    const Partial q = pbase[i];
+    if (better(q.score, q.index, fs, fi)) { fs = q.score; fv = q.value; fi = q.index; }
+  }
+  wave_best(fs, fv, fi);
+  if (lane == 0) {
+    Partial *r = A.results + (int64_t)s * A.n_hp + hp;
+    if (!(A.accumulate && better(r->score, r->index, fs, fi))) *r = Partial{fs, fv, fi, 1, 0};
   }
 }
 
@@ -1017,14 +1154,15 @@ hipError_t launch_split(const double *losses, int64_t n, int32_t n_below, uint8_
 }
 
 hipError_t launch_fit(const tpe_hp *hps, int32_t n_hp, const double *vals,
-                      const uint8_t *active, const uint8_t *below, int64_t n,
+                      const uint8_t *active, const double *losses, int64_t n, int32_t n_below,
                       double prior_weight, int32_t lf, const double *pprior, double *mw,
-                      double *mmu, double *msig, MixInfo *info, int64_t kcap,
-                      double *scratch, hipStream_t st) {
+                      double *mmu, double *msig, MixInfo *info, Coef *coef, int64_t kcap,
+                      double *scratch, double *scratch2, hipStream_t st) {
   if (n_hp <= 0) return hipSuccess;
   const size_t lds = (size_t)12288 * 8;  // 96 KB: see the k_fit LDS layout
-  k_fit<<<dim3(n_hp, 2), 1024, lds, st>>>(hps, vals, active, below, n, prior_weight, lf,
-                                          pprior, mw, mmu, msig, info, kcap, scratch);
+  k_fit<<<dim3(n_hp, 2), 1024, lds, st>>>(hps, vals, active, losses, n, n_below, prior_weight, lf,
+                                          pprior, mw, mmu, msig, info, coef, kcap, scratch,
+                                          scratch2);
   return hipGetLastError();
 }
 
@@ -1059,10 +1197,10 @@ hipError_t launch_draw(const ScoreArgs &a, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_sort_cand(const ScoreArgs &a, int32_t *pos_out, hipStream_t st) {
+hipError_t launch_bucket(const ScoreArgs &a, int32_t *pos_out, hipStream_t st) {
   if (a.n_slots <= 0 || a.n_suggest <= 0 || a.n_cand <= 0) return hipSuccess;
   const unsigned gx = (unsigned)((a.n_cand + kSortMax - 1) / kSortMax);
-  k_sort_cand<<<dim3(gx, a.n_slots, a.n_suggest), 1024, (size_t)kSortMax * 12, st>>>(a, pos_out);
+  k_bucket<<<dim3(gx, a.n_slots, a.n_suggest), 1024, (size_t)kSortMax * 9, st>>>(a, pos_out);
   return hipGetLastError();
 }
 

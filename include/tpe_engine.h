@@ -172,6 +172,12 @@ int tpe_plan_suggest(tpe_plan_t p, const uint64_t *seeds, int64_t n_suggest,
                      int64_t n_cand, int64_t cand_begin, int32_t level,
                      tpe_result *out, int32_t out_on_device, void *stream);
 
+/* Results [n_suggest][n_hp] of the last tpe_plan_suggest (copy), and the
+ * device address where the plan keeps them (valid until the next call).   */
+int tpe_plan_get_results(tpe_plan_t p, tpe_result *out, int32_t out_on_device,
+                         void *stream);
+const tpe_result *tpe_plan_results_device(tpe_plan_t p);
+
 /* Multi-device: combine world copies of one level's results ([world][S][P],
  * device memory, e.g. an RCCL all-gather) with numpy argmax semantics and
  * make them the plan's state.                                              */
