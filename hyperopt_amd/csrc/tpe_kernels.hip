@@ -22,6 +22,14 @@
 
 namespace tpe {
 
+#ifdef TPE_STAMPS
+// debug build only: per-block phase timestamps of k_fit (wall clock, 100 MHz)
+__device__ unsigned long long g_stamps[512][16];
+#define STAMP(slot, ph) do { if (threadIdx.x == 0) g_stamps[(slot) & 511][ph] = wall_clock64(); } while (0)
+#else
+#define STAMP(slot, ph) do {} while (0)
+#endif
+
 // ------------------------------------------------------------------------
 // numpy-compatible scalar helpers
 // ------------------------------------------------------------------------
@@ -367,6 +375,7 @@ __global__ __launch_bounds__(1024) void k_fit(
   double *ob = scratch + slot * kcap;  // observations in tid order
   const double *row = vals + (int64_t)hp * n;
   const uint8_t *arow = active + (int64_t)hp * n;
+  STAMP(slot, 0);
   // ---- good/bad split: threshold key of the n_below best losses
   if (threadIdx.x < 64) {
     double tv;
@@ -377,6 +386,7 @@ __global__ __launch_bounds__(1024) void k_fit(
   __syncthreads();
   const double tv = thr_v;
   const int64_t ti = thr_i;
+  STAMP(slot, 1);
 
   // ---- gather this side's observations, keeping tid order (tpe.py:629-636)
   int m = 0;
@@ -393,6 +403,7 @@ __global__ __launch_bounds__(1024) void k_fit(
     m += tot;
   }
   __syncthreads();
+  STAMP(slot, 2);
   // LDS layout (96 KB): m <= kSortMax -> key[8192] f64 + pos[8192] i32;
   // otherwise an LDS copy of the observations when <= 12288 of them fit.
   const bool small = m <= kSortMax;
@@ -404,6 +415,7 @@ __global__ __launch_bounds__(1024) void k_fit(
   } else {
     sob = ob;
   }
+  STAMP(slot, 3);
 
   if (H.family == TPE_CAT) {
     // LF-weighted bincount in observation order (np.bincount) + pseudocounts.
@@ -434,6 +446,7 @@ __global__ __launch_bounds__(1024) void k_fit(
       w[c] = pc;
     }
     __syncthreads();
+    STAMP(slot, 4);
     const double tot = block_np_sum(w, upper, sm.np);
     for (int c = threadIdx.x; c < upper; c += blockDim.x) {
       w[c] = w[c] / tot;
@@ -443,6 +456,8 @@ __global__ __launch_bounds__(1024) void k_fit(
     if (threadIdx.x == 0) { info[slot].K = upper; info[slot].kind = 2; }
     __syncthreads();
     prep_slot(H, slot, w, mu, sg, info, coef, kcap, scratch2, sm.np);
+    __syncthreads();
+    STAMP(slot, 10);
     return;
   }
 
@@ -504,6 +519,7 @@ __global__ __launch_bounds__(1024) void k_fit(
     }
     if (threadIdx.x == 0) { mu[pos] = pm; w[pos] = prior_weight; }
     __syncthreads();
+    STAMP(slot, 4);
     const int K = m + 1;
     for (int k = threadIdx.x; k < K; k += blockDim.x) {
       double s;
@@ -523,11 +539,15 @@ __global__ __launch_bounds__(1024) void k_fit(
   __syncthreads();
   if (threadIdx.x == 0) sg[pos] = ps;
   __syncthreads();
+  STAMP(slot, 5);
   const double tot = block_np_sum(w, K, sm.np);
   for (int k = threadIdx.x; k < K; k += blockDim.x) w[k] = w[k] / tot;
   if (threadIdx.x == 0) { info[slot].K = K; info[slot].kind = 0; }
   __syncthreads();
+  STAMP(slot, 6);
   prep_slot(H, slot, w, mu, sg, info, coef, kcap, scratch2, sm.np);
+  __syncthreads();
+  STAMP(slot, 10);
 }
 
 // ------------------------------------------------------------------------
@@ -549,6 +569,7 @@ __device__ void prep_slot(const tpe_hp &H, int64_t slot, const double *w, const 
   Coef *cf = coef + slot * kcap;
   double *tmp = scratch + slot * kcap;
   const double wsum = block_np_sum(w, K, np);
+  STAMP(slot, 7);
   if (H.family == TPE_CAT) {
     for (int k = threadIdx.x; k < K; k += blockDim.x) {
       Coef c; c.x = log(w[k]); c.y = 0.0; c.z = 0.0; c.w = 0.0;
@@ -558,6 +579,8 @@ __device__ void prep_slot(const tpe_hp &H, int64_t slot, const double *w, const 
       info[slot].kind = 2; info[slot].p_accept = 1.0; info[slot].log_pacc = 0.0;
       info[slot].wsum = wsum;
     }
+    __syncthreads();
+    STAMP(slot, 9);
     return;
   }
   const bool bounded = (H.flags & (TPE_HAS_LOW | TPE_HAS_HIGH)) != 0;
@@ -568,6 +591,7 @@ __device__ void prep_slot(const tpe_hp &H, int64_t slot, const double *w, const 
     __syncthreads();
     pacc = block_np_sum(tmp, K, np);
   }
+  STAMP(slot, 8);
   const bool quant = (H.flags & TPE_HAS_Q) != 0;
   const double L2E = 1.4426950408889634;  // log2(e)
   const double A0 = sqrt(0.5 * L2E);
@@ -1133,6 +1157,14 @@ __global__ __launch_bounds__(256) void k_micro(int iters, double *sink) {
     if (acc == 12345.0) sink[t] = acc;
   }
 }
+
+#ifdef TPE_STAMPS
+}  // namespace tpe
+extern "C" int tpe_debug_stamps(unsigned long long *out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(tpe::g_stamps), sizeof(tpe::g_stamps)) == hipSuccess ? 0 : -5;
+}
+namespace tpe {
+#endif
 
 hipError_t launch_micro(int which, int blocks, int iters, double *sink, hipStream_t st) {
   switch (which) {

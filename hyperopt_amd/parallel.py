@@ -1,0 +1,138 @@
+"""Multi-GPU TPE suggestion: one process per GPU over torch.distributed.
+
+Two ways the suggest path shards:
+
+* **Batched asynchronous suggestions** (config 5): every rank serves its own
+  suggestions (distinct seeds) on the same history.  Nothing is exchanged:
+  :func:`suggestion_slice` only decides which seeds a rank owns.
+
+* **One suggestion sharded over ranks** (configs 2-4): rank r draws and
+  scores the global candidate range :func:`shard_range` of every hp.  The
+  device draws are counter-based (Philox keyed by seed, counter = global
+  candidate index), so the union of the shards is exactly the candidate set
+  of the unsharded suggest.  After each conditional level the per-hp
+  ``(score, value, index)`` winners (32-byte ``tpe_result`` records,
+  [S][P]) are all-gathered -- RCCL over xGMI on GPU, gloo in the CPU tests --
+  and merged on the device by ``tpe_plan_merge`` with numpy argmax semantics
+  (first maximum, a NaN wins at its first index, tpe.py:756), so the next
+  level's activity test and the returned values are identical to one GPU's.
+
+RCCL has no max-loc reduction; an all-gather of G x S x P x 32 bytes followed
+by a deterministic device merge is both exact and, at these sizes
+(kilobytes), latency-bound at one collective per level.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _engine as E
+
+RECORD_BYTES = E.RESULT_DTYPE.itemsize  # sizeof(tpe_result) == 32
+
+
+def shard_range(n: int, rank: int, world: int):
+    """(begin, count) of rank's share of [0, n): contiguous, balanced to
+    within one candidate, covering [0, n) exactly once over all ranks."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError('bad rank/world %r/%r' % (rank, world))
+    if n < 0:
+        raise ValueError('n < 0')
+    base, extra = divmod(n, world)
+    begin = rank * base + min(rank, extra)
+    return begin, base + (1 if rank < extra else 0)
+
+
+def suggestion_slice(n_suggest: int, rank: int, world: int):
+    """Suggestion indices a rank serves in batched asynchronous mode."""
+    b, c = shard_range(n_suggest, rank, world)
+    return range(b, b + c)
+
+
+def gather_records(local, group=None):
+    """All-gather a rank's flat byte tensor of result records.
+
+    Returns one contiguous tensor [world * local.numel()] in rank order, the
+    [world][S][P] layout ``tpe_plan_merge`` expects.  Uses the fused
+    ``all_gather_into_tensor`` (one RCCL call) where the backend has it and a
+    list all-gather otherwise (gloo on CPU)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    if local.is_cuda and dist.get_backend(group) == 'nccl':
+        out = torch.empty(world * local.numel(), dtype=local.dtype, device=local.device)
+        dist.all_gather_into_tensor(out, local, group=group)
+        return out
+    # gloo: stage through host memory (CPU tests; several ranks on one GPU)
+    src = local.cpu()
+    parts = [torch.empty_like(src) for _ in range(world)]
+    dist.all_gather(parts, src, group=group)
+    return torch.cat(parts).to(local.device)
+
+
+def merge_records_host(gathered: np.ndarray) -> np.ndarray:
+    """Host restatement of k_merge for tests and diagnostics only: combine
+    [world][S][P] records with numpy argmax semantics.  The product path
+    merges on the device (ShardedSuggest)."""
+    world, S, P = gathered.shape
+    out = np.empty((S, P), dtype=E.RESULT_DTYPE)
+    for s in range(S):
+        for p in range(P):
+            best = None
+            active = 0
+            for r in range(world):
+                q = gathered[r, s, p]
+                active |= int(q['active'])
+                if q['index'] < 0:
+                    continue
+                if best is None or _better(q, best):
+                    best = q
+            if best is None or not active:
+                out[s, p] = (np.nan, np.nan, -1, active, 0)
+            else:
+                out[s, p] = (best['score'], best['value'], best['index'], 1, 0)
+    return out
+
+
+def _better(a, b):
+    na, nb = np.isnan(a['score']), np.isnan(b['score'])
+    if na or nb:
+        return a['index'] < b['index'] if (na and nb) else bool(na)
+    if a['score'] != b['score']:
+        return a['score'] > b['score']
+    return a['index'] < b['index']
+
+
+class ShardedSuggest(object):
+    """One suggestion's candidates sharded over the ranks of ``group``.
+
+    ``plan`` is this rank's :class:`hyperopt_amd._engine.Plan` (same space,
+    same history, fitted); the engine enqueues on torch's current stream so
+    the gather is ordered after the scoring and the merge after the gather.
+    """
+
+    def __init__(self, plan, group=None):
+        import torch
+        import torch.distributed as dist
+        self.plan = plan
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.device = torch.device('cuda', plan.engine.device)
+        self.gather = lambda t: gather_records(t, self.group)
+
+    def suggest(self, seeds, n_cand, fetch=True):
+        import torch
+        seeds = np.ascontiguousarray(np.atleast_1d(seeds), dtype=np.uint64)
+        S, P = seeds.size, self.plan.n_hp
+        begin, count = shard_range(int(n_cand), self.rank, self.world)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        local = torch.empty(S * P * RECORD_BYTES, dtype=torch.uint8, device=self.device)
+        for level in range(self.plan.n_levels):
+            self.plan.suggest(seeds, count, cand_begin=begin, level=level, out=local.data_ptr(),
+                              stream=stream)
+            gathered = self.gather(local)
+            self.plan.merge(gathered.data_ptr(), self.world, level, out=local.data_ptr(),
+                            stream=stream, n_suggest=S)
+        if not fetch:
+            return local
+        return local.cpu().numpy().view(E.RESULT_DTYPE).reshape(S, P)
