@@ -44,6 +44,8 @@ struct tpe_plan {
   double *d_losses = nullptr, *d_vals = nullptr;
   uint8_t *d_active = nullptr, *d_below = nullptr;
   double *d_mw = nullptr, *d_mmu = nullptr, *d_msig = nullptr, *d_scratch = nullptr;
+  unsigned char *d_sortbuf = nullptr;  // [2P][16 * scap] fit sort scratch
+  int64_t scap = 0;
   MixInfo *d_info = nullptr;
   Coef *d_coef = nullptr;
   int64_t n = 0;  // history length
@@ -111,7 +113,7 @@ void plan_free_buffers(tpe_plan *p) {
                   p->d_losses, p->d_vals, p->d_active, p->d_below, p->d_mw, p->d_mmu,
                   p->d_msig, p->d_scratch, p->d_info, p->d_coef, p->d_results, p->d_seeds,
                   p->d_partial, p->d_ext, p->d_lb, p->d_la, p->d_cand, p->d_cpos,
-                  p->d_ticket};
+                  p->d_ticket, p->d_sortbuf};
   for (void *b : bufs) dfree(b);
   if (p->ev0) (void)hipEventDestroy(p->ev0);
   if (p->ev1) (void)hipEventDestroy(p->ev1);
@@ -236,6 +238,8 @@ int plan_build(tpe_engine *h, const tpe_space *sp, int64_t max_trials, tpe_plan 
   CKH(dalloc(&p->d_mmu, (size_t)slots * kcap));
   CKH(dalloc(&p->d_msig, (size_t)slots * kcap));
   CKH(dalloc(&p->d_scratch, (size_t)slots * kcap));
+  p->scap = p->ncap + 1;
+  CKH(dalloc(&p->d_sortbuf, (size_t)slots * 16 * p->scap));
   CKH(dalloc(&p->d_info, slots));
   CKH(dalloc(&p->d_coef, (size_t)slots * kcap));
   CKH(hipEventCreate(&p->ev0));
@@ -355,6 +359,30 @@ ScoreArgs base_args(tpe_plan *p, int64_t n_sug) {
   a.kcap = p->kcap;
   a.n_hp = p->P;
   a.n_suggest = (int32_t)n_sug;
+  return a;
+}
+
+FitArgs fit_args(tpe_plan *p, int32_t n_below, double prior_weight, int32_t lf) {
+  FitArgs a{};
+  a.hps = p->d_hps;
+  a.vals = p->d_vals;
+  a.active = p->d_active;
+  a.losses = p->d_losses;
+  a.n = p->n;
+  a.n_below = n_below;
+  a.lf = lf;
+  a.prior_weight = prior_weight;
+  a.pprior = p->d_pprior;
+  a.mw = p->d_mw;
+  a.mmu = p->d_mmu;
+  a.msig = p->d_msig;
+  a.info = p->d_info;
+  a.coef = p->d_coef;
+  a.kcap = p->kcap;
+  a.ob = p->d_scratch;
+  a.tmp = p->d_scratch;
+  a.sortbuf = p->d_sortbuf;
+  a.scap = p->scap;
   return a;
 }
 
@@ -596,7 +624,8 @@ int tpe_split(tpe_handle_t h, const double *losses, int64_t n, double gamma,
   if (rc) return rc;
   const int32_t nb = (int32_t)std::min<double>(std::ceil(gamma * std::sqrt((double)n)), gamma_cap);
   CKH(hipMemcpyAsync(p->d_losses, losses, n * 8, hipMemcpyHostToDevice, h->stream));
-  CKH(launch_split(p->d_losses, n, std::max(nb, 0), p->d_below, h->stream));
+  p->n = n;
+  CKH(launch_split(fit_args(p, std::max(nb, 0), 1.0, 25), p->d_below, h->stream));
   CKH(hipMemcpyAsync(below_mask, p->d_below, n, hipMemcpyDeviceToHost, h->stream));
   CKH(hipStreamSynchronize(h->stream));
   return TPE_OK;
@@ -623,9 +652,8 @@ static int fit_one(tpe_handle_t h, int32_t family, const double *obs, int64_t n,
     CKH(hipMemsetAsync(p->d_below, 1, n, h->stream));
   }
   if (n > 0) CKH(hipMemsetAsync(p->d_losses, 0, n * 8, h->stream));
-  CKH(launch_fit(p->d_hps, 1, p->d_vals, p->d_active, p->d_losses, n, (int32_t)n, prior_weight,
-                 lf, p->d_pprior, p->d_mw, p->d_mmu, p->d_msig, p->d_info, p->d_coef, p->kcap,
-                 p->d_scratch, p->d_scratch, h->stream));
+  p->n = n;
+  CKH(launch_fit(fit_args(p, (int32_t)n, prior_weight, lf), 1, h->stream));
   *pout = p;
   return TPE_OK;
 }
@@ -819,9 +847,7 @@ int tpe_plan_fit(tpe_plan_t p, double gamma, int32_t gamma_cap, double prior_wei
   hipStream_t st = pick_stream(h, stream);
   const double nbf = std::ceil(gamma * std::sqrt((double)p->n));
   const int32_t nb = (int32_t)std::max(0.0, std::min<double>(nbf, gamma_cap));
-  CKH(launch_fit(p->d_hps, p->P, p->d_vals, p->d_active, p->d_losses, p->n, nb, prior_weight, lf,
-                 p->d_pprior, p->d_mw, p->d_mmu, p->d_msig, p->d_info, p->d_coef, p->kcap,
-                 p->d_scratch, p->d_scratch, st));
+  CKH(launch_fit(fit_args(p, nb, prior_weight, lf), p->P, st));
   return TPE_OK;
 }
 

@@ -1,0 +1,1049 @@
+// tpe_fit.hip -- good/bad split, adaptive Parzen fit / categorical posterior
+// and per-component lpdf constants of every (hp, side) slot, gfx950.
+//
+// Reference (pminervini/hyperopt, hyperopt/tpe.py):
+//   ap_filter_trials            tpe.py:613-641   split_threshold / gather
+//   linear_forgetting_weights   tpe.py:381-394   lf_weight
+//   adaptive_parzen_normal      tpe.py:398-475   fit_continuous
+//   ap_categorical_sampler      tpe.py:573-607   fit_categorical
+//   GMM1_lpdf / LGMM1_lpdf      tpe.py:104-166, 259-301: per-component
+//                               constants + p_accept (prep_slot)
+//
+// One 1024-thread block per (hp, side).  Everything a block touches more than
+// once lives in LDS (160 KB on gfx950): the sort keys and permutations, and
+// for K <= kMixLds the whole mixture until the final copy-out.  The sort is a
+// stable LSD radix sort of the permutation over 8-bit digits of a 64-bit key
+// (digits that are equal for every key are skipped), with wave-level ballot
+// ranking, so its cost is a few passes of ~2 barriers each instead of the
+// O(log^2 n) barrier stages of a bitonic network.  Every floating-point
+// operation that reaches the outputs is the reference's own, in its order
+// (numpy pairwise summation included), so the fit is bit-identical to the
+// reference whenever the reference's argsort has no ties to reorder.
+#include <math.h>
+
+#include "tpe_device.hpp"
+
+#pragma clang fp contract(off)
+
+namespace tpe {
+
+// k_fit runs once per CU per suggest, so its cost is dominated by first-time
+// instruction fetch: helpers called several times per block are kept out of
+// line (NOINLINE) so later calls run from a warm instruction cache.
+#define NOINLINE __attribute__((noinline))
+
+#ifdef TPE_STAMPS
+// diagnostic build only (make dbg; tools/fit_stamps.py): per-slot phase
+// timestamps of k_fit, wall clock (100 MHz)
+__device__ unsigned long long g_stamps[512][16];
+#define STAMP(ph)                                                             \
+  do {                                                                        \
+    if (threadIdx.x == 0 && blockIdx.z == 0)                                  \
+      g_stamps[(2 * blockIdx.x + blockIdx.y) & 511][ph] = wall_clock64();     \
+  } while (0)
+#else
+#define STAMP(ph) do {} while (0)
+#endif
+
+constexpr int kFitWaves = kFitThreads / 64;  // 16
+constexpr int kSortCap = 10000;              // elements sorted in LDS (u16 positions)
+constexpr int kMixLds = 4097;                // K kept in LDS until copy-out (m <= 4096)
+constexpr int kMixStride = 4104;             // doubles per LDS mixture array
+constexpr int kDigits = 256;
+
+// dynamic LDS map (bytes)
+constexpr int kOffKeys = 0;                               // u64 [kSortCap]
+constexpr int kOffPosA = kOffKeys + 8 * kSortCap;         // u16 [kSortCap]
+constexpr int kOffPosB = kOffPosA + 2 * kSortCap;         // u16 [kSortCap]
+constexpr int kOffCnt = kOffPosB + 2 * kSortCap;          // u32 [256][16]
+constexpr int kOffRun = kOffCnt + 4 * kDigits * kFitWaves;  // u32 [16][256]
+constexpr int kFitLds = kOffRun + 4 * kDigits * kFitWaves;  // 155,648 B
+static_assert(4 * 8 * kMixStride <= kFitLds, "LDS mixture arrays");
+
+// numpy pairwise_sum tree of one chunk length n (<= 8192): leaves of <= 128
+// elements, internal node = left + right with left = floor(n/2) rounded down
+// to a multiple of 8.  Built breadth-first by one wave (lanes = nodes of a
+// level) and evaluated bottom-up level by level by one wave, so neither the
+// planning nor the combine is a serial recursion.
+constexpr int kNpNodes = 2 * kMaxLeaves;
+struct NpPlan {
+  int n, n_leaves, n_int, levels;
+  uint16_t leaf_lo[kMaxLeaves], leaf_n[kMaxLeaves], leaf_id[kMaxLeaves];
+  uint16_t int_lo[kMaxLeaves], int_n[kMaxLeaves], int_id[kMaxLeaves], int_cid[kMaxLeaves];
+  uint16_t lvl_begin[16];  // internal nodes of level d: [lvl_begin[d], lvl_begin[d + 1])
+};
+
+struct FitShared {
+  NpPlan np;                 // pairwise-sum tree of the last chunk length
+  double val[2][kNpNodes];   // node sums (two arrays summed together)
+  double total2[2];
+  uint64_t rk[2][kFitWaves];
+  uint32_t rp[2][kFitWaves];
+  uint64_t vand[kFitWaves], vor[kFitWaves];
+  int wsum[kFitWaves + 1];
+  int isum[kFitWaves];
+  int m, nlt;
+};
+
+// ------------------------------------------------------------------------
+// wave / block primitives
+// ------------------------------------------------------------------------
+__device__ __forceinline__ void wave_min_kp(uint64_t &k, uint32_t &p) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t ok = __shfl_xor(k, o, 64);
+    const uint32_t op = __shfl_xor(p, o, 64);
+    if (kp_less(ok, op, k, p)) { k = ok; p = op; }
+  }
+}
+
+__device__ __forceinline__ uint32_t wave_excl_scan_u32(uint32_t v) {
+  const int lane = threadIdx.x & 63;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  return x - v;
+}
+
+// block-wide sum of small ints (one barrier pair)
+__device__ int block_sum_int(int v, int *buf) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if (lane == 0) buf[w] = v;
+  __syncthreads();
+  int t = 0;
+#pragma unroll
+  for (int i = 0; i < kFitWaves; ++i) t += buf[i];
+  __syncthreads();
+  return t;
+}
+
+// block-wide exclusive scan of small ints; total returned by reference
+__device__ NOINLINE int block_excl_scan(int v, int *wsum, int &total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  int before = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < kFitWaves; ++i) {
+    const int s = wsum[i];
+    before += (i < w) ? s : 0;
+    tot += s;
+  }
+  total = tot;
+  __syncthreads();
+  return before + x - v;
+}
+
+// lanes of this wave whose 8-bit digit equals mine (among lanes with v set)
+__device__ __forceinline__ uint64_t match8(uint32_t d, bool v) {
+  uint64_t m = __ballot(v);
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    const bool s = (d >> b) & 1u;
+    const uint64_t bb = __ballot(s);
+    m &= s ? bb : ~bb;
+  }
+  return m;
+}
+
+__device__ __forceinline__ uint64_t lanemask_lt() {
+  const int lane = threadIdx.x & 63;
+  return lane ? (~0ull >> (64 - lane)) : 0ull;
+}
+
+// ------------------------------------------------------------------------
+// stable LSD radix sort of a permutation (ascending key, ties keep the
+// initial order = position).  keys[] indexed by element id; a/b: LDS (u16)
+// or global (u32) permutations; cnt/run: 16 KB each in LDS.  Returns the
+// buffer holding the sorted permutation.
+// ------------------------------------------------------------------------
+template <typename PosT>
+__device__ NOINLINE void radix_pass(const uint64_t *keys, const PosT *a, PosT *b, int n, int shift,
+                           uint32_t *cnt, uint32_t *run) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int per = ((n + kFitWaves * 64 - 1) / (kFitWaves * 64)) * 64;  // slots per wave
+  const int r0 = w * per, r1 = min(n, r0 + per);
+  uint32_t *mycnt = cnt + w * kDigits;  // wave-private row while counting
+  for (int d = lane; d < kDigits; d += 64) mycnt[d] = 0;
+  for (int base = r0; base < r1; base += 64) {
+    const int r = base + lane;
+    const bool v = r < r1;
+    const uint32_t d = v ? (uint32_t)(keys[a[r]] >> shift) & 255u : 0u;
+    const uint64_t mt = match8(d, v);
+    if (v && lane == __ffsll((long long)mt) - 1) mycnt[d] += __popcll(mt);
+  }
+  __syncthreads();
+  // this wave's base for every digit: exclusive prefix over (digit, wave).
+  // Lane l owns digits 4l..4l+3: one conflict-free 16-byte read per wave row.
+  uint32_t tot[4] = {0u, 0u, 0u, 0u}, mine[4] = {0u, 0u, 0u, 0u};
+#pragma unroll 2
+  for (int i = 0; i < kFitWaves; ++i) {
+    const uint4 c = *reinterpret_cast<const uint4 *>(cnt + i * kDigits + 4 * lane);
+    const uint32_t below = (i < w) ? 1u : 0u;
+    tot[0] += c.x; tot[1] += c.y; tot[2] += c.z; tot[3] += c.w;
+    mine[0] += below * c.x; mine[1] += below * c.y; mine[2] += below * c.z; mine[3] += below * c.w;
+  }
+  const uint32_t ls = tot[0] + tot[1] + tot[2] + tot[3];
+  uint32_t acc = wave_excl_scan_u32(ls);
+  uint32_t *myrun = run + w * kDigits;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    myrun[4 * lane + q] = acc + mine[q];
+    acc += tot[q];
+  }
+  // stable scatter (wave-private running bases, LDS ops in program order)
+  for (int base = r0; base < r1; base += 64) {
+    const int r = base + lane;
+    const bool v = r < r1;
+    const PosT e = v ? a[r] : (PosT)0;
+    const uint32_t d = v ? (uint32_t)(keys[e] >> shift) & 255u : 0u;
+    const uint64_t mt = match8(d, v);
+    const uint32_t rank = __popcll(mt & lanemask_lt());
+    const uint32_t bs = v ? myrun[d] : 0u;
+    if (v) b[bs + rank] = e;
+    if (v && lane == __ffsll((long long)mt) - 1) myrun[d] = bs + __popcll(mt);
+  }
+  __syncthreads();
+}
+
+// ------------------------------------------------------------------------
+// 64 < n <= 1024 (keys in LDS): each wave sorts a run of 64 (key, position)
+// pairs in registers (bitonic network over shuffles), then runs are merged
+// pairwise in LDS (4 levels): an element's index in the merged run is its
+// index in its own run plus its lower bound in the partner run.
+// ------------------------------------------------------------------------
+constexpr int kMergeMax = 1024;
+
+__device__ void wave_bitonic64(uint64_t &k, uint32_t &p) {
+  const int lane = threadIdx.x & 63;
+  // loops kept rolled: k_fit runs once per CU, so code size is latency
+  for (int kk = 2; kk <= 64; kk <<= 1) {
+    for (int j = kk >> 1; j > 0; j >>= 1) {
+      const bool asc = (lane & kk) == 0 || kk == 64;
+      const uint64_t ok = __shfl_xor(k, j, 64);
+      const uint32_t op = __shfl_xor(p, j, 64);
+      const bool lower = (lane & j) == 0;
+      const bool other_less = kp_less(ok, op, k, p);
+      // the lower slot keeps the min when ascending, the max when descending
+      if ((lower == asc) ? other_less : !other_less) { k = ok; p = op; }
+    }
+  }
+}
+
+__device__ void merge_sort_1024(const uint64_t *keys, int n, uint16_t *out, uint64_t *bk0,
+                                uint16_t *bp0, uint64_t *bk1, uint16_t *bp1) {
+  const int t = threadIdx.x;
+  uint64_t k = t < n ? keys[t] : ~0ull;
+  uint32_t p = (uint32_t)t;  // padding (~0, t >= n): distinct, after every real key
+  wave_bitonic64(k, p);
+  bk0[t] = k;
+  bp0[t] = (uint16_t)p;
+  __syncthreads();
+  uint64_t *sk = bk0, *dk = bk1;
+  uint16_t *sp = bp0, *dp = bp1;
+  for (int len = 64; len < kFitThreads; len <<= 1) {
+    const int run = t / len, idx = t % len;
+    const int other = (run ^ 1) * len;
+    int lo = 0, hi = len;  // lower bound of (k, p) in the partner run
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (kp_less(sk[other + mid], sp[other + mid], k, p)) lo = mid + 1;
+      else hi = mid;
+    }
+    const int dst = (run & ~1) * len + idx + lo;
+    dk[dst] = k;
+    dp[dst] = (uint16_t)p;
+    __syncthreads();
+    uint64_t *tk = sk; sk = dk; dk = tk;
+    uint16_t *tp = sp; sp = dp; dp = tp;
+    k = sk[t];  // this thread now owns merged position t
+    p = sp[t];
+  }
+  if (t < n) out[t] = sp[t];
+  __syncthreads();
+}
+
+template <typename PosT>
+__device__ PosT *block_sort_perm(const uint64_t *keys, PosT *a, PosT *b, int n, uint32_t *cnt,
+                                 uint32_t *run, FitShared &sm) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (n > 64 && n <= kMergeMax && sizeof(PosT) == 2) {
+    // cnt + run regions (32 KB) hold the two key buffers, b the positions
+    uint64_t *bk = reinterpret_cast<uint64_t *>(cnt);
+    uint16_t *bp = reinterpret_cast<uint16_t *>(b);
+    merge_sort_1024(keys, n, reinterpret_cast<uint16_t *>(a), bk, bp, bk + kFitThreads,
+                    bp + kFitThreads);
+    return a;
+  }
+  if (n <= 64) {  // one wave: rank by counting, no barriers inside
+    if (w == 0 && lane < n) {
+      const uint64_t k = keys[lane];
+      int rank = 0;
+      for (int j = 0; j < n; ++j) rank += kp_less(keys[j], j, k, lane) ? 1 : 0;
+      a[rank] = (PosT)lane;
+    }
+    __syncthreads();
+    return a;
+  }
+  uint64_t an = ~0ull, on = 0ull;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    a[i] = (PosT)i;
+    const uint64_t k = keys[i];
+    an &= k;
+    on |= k;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    an &= __shfl_xor(an, o, 64);
+    on |= __shfl_xor(on, o, 64);
+  }
+  if (lane == 0) { sm.vand[w] = an; sm.vor[w] = on; }
+  __syncthreads();
+  an = ~0ull;
+  on = 0ull;
+#pragma unroll
+  for (int i = 0; i < kFitWaves; ++i) { an &= sm.vand[i]; on |= sm.vor[i]; }
+  const uint64_t vary = an ^ on;
+  for (int shift = 0; shift < 64; shift += 8) {
+    if (((vary >> shift) & 255u) == 0) continue;
+    radix_pass<PosT>(keys, a, b, n, shift, cnt, run);
+    PosT *t = a; a = b; b = t;
+  }
+  return a;
+}
+
+// ------------------------------------------------------------------------
+// numpy float64 sum (ndarray.sum): buffers of 8192 elements, each reduced by
+// pairwise_sum (leaves of <= 128 with 8 accumulators, split at n/2 rounded
+// down to a multiple of 8), buffer results added in order.  Leaves run in
+// parallel on 8-lane groups, lane s owning numpy's accumulator r[s].
+// ------------------------------------------------------------------------
+// wave 0: breadth-first construction of the tree of length n
+__device__ NOINLINE void np_plan(int n, NpPlan &P) {
+  const int lane = threadIdx.x & 63;
+  int nl = 0, ni = 0, next_id = 1, lvl = 0;
+  // root
+  if (n <= 128) {
+    if (lane == 0) { P.leaf_lo[0] = 0; P.leaf_n[0] = (uint16_t)n; P.leaf_id[0] = 0; }
+    nl = 1;
+  } else {
+    if (lane == 0) { P.int_lo[0] = 0; P.int_n[0] = (uint16_t)n; P.int_id[0] = 0; P.lvl_begin[0] = 0; }
+    ni = 1;
+  }
+  int b0 = 0, b1 = ni;  // internal nodes of the current level
+  while (b1 > b0) {
+    if (lane == 0) P.lvl_begin[lvl] = (uint16_t)b0;
+    // children of this level's internal nodes, in order; 4 parents per lane max
+    int add_l = 0, add_i = 0;
+    for (int c0 = b0; c0 < b1; c0 += 64) {
+      const int c = c0 + lane;
+      const bool v = c < b1;
+      int off = 0, m = 0;
+      if (v) { off = P.int_lo[c]; m = P.int_n[c]; }
+      int n2 = m / 2;
+      n2 -= n2 % 8;
+      const int cl_off = off, cl_n = n2, cr_off = off + n2, cr_n = m - n2;
+      const bool lleaf = v && cl_n <= 128, rleaf = v && cr_n <= 128;
+      const bool lint = v && !lleaf, rint = v && !rleaf;
+      // child ids: 2 per parent, in parent order (left, right)
+      const int my_ids = v ? 2 : 0;
+      const int id_base = next_id + (int)wave_excl_scan_u32((uint32_t)my_ids);
+      const int lp = (int)wave_excl_scan_u32((uint32_t)(lleaf + rleaf));
+      const int ip = (int)wave_excl_scan_u32((uint32_t)(lint + rint));
+      int li = nl + add_l + lp, ii = b1 + add_i + ip;
+      if (v) {
+        const int idl = id_base, idr = id_base + 1;
+        P.int_cid[c] = (uint16_t)idl;
+        // left child first, then right (order inside a level is free)
+        if (lleaf) { P.leaf_lo[li] = cl_off; P.leaf_n[li] = cl_n; P.leaf_id[li] = idl; ++li; }
+        else { P.int_lo[ii] = cl_off; P.int_n[ii] = cl_n; P.int_id[ii] = idl; ++ii; }
+        if (rleaf) { P.leaf_lo[li] = cr_off; P.leaf_n[li] = cr_n; P.leaf_id[li] = idr; }
+        else { P.int_lo[ii] = cr_off; P.int_n[ii] = cr_n; P.int_id[ii] = idr; }
+      }
+      // totals of this 64-parent batch (lane 63 holds the last prefix)
+      const int last = min(64, b1 - c0) - 1;
+      const int tl = __shfl(lp + (int)(lleaf + rleaf), last, 64);
+      const int ti = __shfl(ip + (int)(lint + rint), last, 64);
+      const int tid = __shfl(id_base + my_ids, last, 64) - next_id;
+      add_l += tl;
+      add_i += ti;
+      next_id += tid;
+    }
+    nl += add_l;
+    b0 = b1;
+    b1 = b1 + add_i;
+    ++lvl;
+  }
+  if (lane == 0) {
+    P.n = n; P.n_leaves = nl; P.n_int = b1; P.levels = lvl; P.lvl_begin[lvl] = (uint16_t)b1;
+  }
+}
+
+// wave 0: bottom-up evaluation of the tree (node = left + right)
+template <int NA>
+__device__ __forceinline__ void np_combine_wave(const NpPlan &P, double (&val)[2][kNpNodes]) {
+  const int lane = threadIdx.x & 63;
+  for (int l = P.levels - 1; l >= 0; --l) {
+    const int c1 = P.lvl_begin[l + 1];
+    for (int c = P.lvl_begin[l] + lane; c < c1; c += 64) {
+      const int id = P.int_id[c], cid = P.int_cid[c];
+#pragma unroll
+      for (int q = 0; q < NA; ++q) val[q][id] = val[q][cid] + val[q][cid + 1];
+    }
+    // LDS ops of one wave complete in order: the next level reads these
+  }
+}
+
+// numpy float64 sum (ndarray.sum) of NA arrays: buffers of 8192 elements,
+// each by the pairwise tree above, buffer results added in order.  Leaves
+// run in parallel on 8-lane groups, lane s owning numpy's accumulator r[s].
+template <int NA>
+__device__ __forceinline__ void block_np_sums(const double *const (&arr)[NA], int64_t n,
+                                              FitShared &sm, double (&out)[NA]) {
+  const int s = threadIdx.x & 7, groups = blockDim.x >> 3;
+  NpPlan &P = sm.np;
+  for (int64_t c0 = 0; c0 < n; c0 += 8192) {
+    const int cn = (int)min<int64_t>(8192, n - c0);
+    __syncthreads();
+    if (threadIdx.x < 64 && P.n != cn) np_plan(cn, P);
+    __syncthreads();
+    const int nl = P.n_leaves;
+    for (int g0 = 0; g0 < nl; g0 += groups) {  // uniform trip count
+      const int g = g0 + (threadIdx.x >> 3);
+      const bool has = g < nl;
+      const int ln = has ? P.leaf_n[g] : 0;
+      const int off = (int)c0 + (has ? P.leaf_lo[g] : 0);
+      const int body = ln - ln % 8;
+#pragma unroll
+      for (int q = 0; q < NA; ++q) {
+        const double *p = arr[q] + off;
+        double r = 0.0;
+        if (ln >= 8) {
+          r = p[s];
+          for (int i = 8 + s; i < body; i += 8) r += p[i];
+        }
+        r = r + __shfl_xor(r, 1, 64);
+        r = r + __shfl_xor(r, 2, 64);
+        r = r + __shfl_xor(r, 4, 64);
+        if (has && s == 0) {
+          double res;
+          if (ln < 8) {
+            res = 0.0;
+            for (int i = 0; i < ln; ++i) res += p[i];
+          } else {
+            res = r;
+            for (int i = body; i < ln; ++i) res += p[i];
+          }
+          sm.val[q][P.leaf_id[g]] = res;
+        }
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      np_combine_wave<NA>(P, sm.val);
+      if (threadIdx.x == 0) {
+#pragma unroll
+        for (int q = 0; q < NA; ++q)
+          sm.total2[q] = (c0 == 0) ? (0.0 + sm.val[q][0]) : (sm.total2[q] + sm.val[q][0]);
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < NA; ++q) out[q] = n > 0 ? sm.total2[q] : 0.0;
+  __syncthreads();
+}
+
+__device__ double block_np_sum(const double *a, int64_t n, FitShared &sm) {
+  const double *const arr[1] = {a};
+  double out[1];
+  block_np_sums<1>(arr, n, sm, out);
+  return out[0];
+}
+
+// ------------------------------------------------------------------------
+// scalar helpers of the reference
+// ------------------------------------------------------------------------
+// linear_forgetting_weights(n, lf)[i] (tpe.py:381-394) with numpy linspace
+// rounding (i*step + start, last ramp element == stop).  The two divisions
+// are hoisted: LfRamp is built once per slot.
+struct LfRamp {
+  int64_t ramp;  // ramp length n - lf (<= 0: all ones)
+  double start, step;
+};
+__device__ __forceinline__ LfRamp lf_ramp(int64_t n, int32_t lf) {
+  LfRamp r;
+  r.ramp = n < lf ? 0 : n - lf;
+  r.start = 1.0 / (double)(n > 0 ? n : 1);
+  r.step = r.ramp > 1 ? (1.0 - r.start) / (double)(r.ramp - 1) : 0.0;
+  return r;
+}
+__device__ __forceinline__ double lf_weight(const LfRamp &r, int64_t i) {
+  if (i >= r.ramp) return 1.0;
+  if (r.ramp == 1) return r.start;
+  if (i == r.ramp - 1) return 1.0;
+  return (double)i * r.step + r.start;
+}
+
+__device__ __forceinline__ double obs_transform(double v, int32_t tf, double low) {
+  switch (tf) {
+    case TPE_OBS_LOG: return log(v);
+    case TPE_OBS_LOG_CLIP_EXPLOW: return log(np_maximum(v, np_maximum(kEPS, exp(low))));
+    case TPE_OBS_LOG_CLIP_EPS: return log(np_maximum(v, kEPS));
+    default: return v;
+  }
+}
+
+// ------------------------------------------------------------------------
+// (a2) split: the n_below-th smallest (loss key, position).  below(j) <=>
+// (key_j, j) <= threshold.  mode 0: nothing below, 1: everything below.
+// ------------------------------------------------------------------------
+struct Split {
+  uint64_t k;
+  uint32_t p;
+  int mode;  // 0 none, 1 all, 2 threshold
+};
+
+__device__ __forceinline__ bool is_below(const Split &t, uint64_t k, uint32_t j) {
+  return t.mode == 1 || (t.mode == 2 && !kp_less(t.k, t.p, k, j));
+}
+
+struct FitCtx {
+  unsigned char *lds;
+  uint64_t *gkeys;      // global sort keys   [scap]
+  uint32_t *gpa, *gpb;  // global permutations [scap]
+};
+
+struct Digit {
+  uint32_t d;    // selected digit
+  uint32_t cnt;  // values with that digit (under the prefix)
+};
+
+// One radix-select step: histogram (wave-aggregated LDS atomics) of the
+// 8-bit digit at `shift` of the values v(j) whose bits under `mask` equal
+// `prefix`, then the digit holding the need-th (1-based) smallest; `need`
+// becomes the rank inside that digit.
+template <typename ValFn>
+__device__ NOINLINE Digit select_digit(ValFn val, int n, uint64_t mask, uint64_t prefix, int shift,
+                              uint32_t &need, uint32_t *hist, FitShared &sm, int par) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // hist[0..256) is zero on entry; zero the other half for the next step
+  // (nobody reads it before this step's first barrier)
+  uint32_t *other = par ? hist - kDigits : hist + kDigits;
+  for (int d = threadIdx.x; d < kDigits; d += blockDim.x) other[d] = 0;
+  for (int j0 = 0; j0 < n; j0 += blockDim.x) {
+    const int j = j0 + threadIdx.x;
+    const uint64_t x = j < n ? val(j) : 0ull;
+    const bool v = j < n && (x & mask) == prefix;
+    const uint32_t d = v ? (uint32_t)(x >> shift) & 255u : 0u;
+    const uint64_t mt = match8(d, v);
+    if (v && lane == __ffsll((long long)mt) - 1) atomicAdd(&hist[d], (uint32_t)__popcll(mt));
+  }
+  __syncthreads();
+  if (w == 0) {
+    const uint4 c = *reinterpret_cast<const uint4 *>(hist + 4 * lane);
+    const uint32_t ls = c.x + c.y + c.z + c.w;
+    const uint32_t before = wave_excl_scan_u32(ls);
+    if (before < need && need <= before + ls) {  // the digit reaching `need`
+      uint32_t acc = before, dd = 4 * lane, cnt = c.x;
+      if (acc + c.x < need) {
+        acc += c.x; dd += 1; cnt = c.y;
+        if (acc + c.y < need) {
+          acc += c.y; dd += 1; cnt = c.z;
+          if (acc + c.z < need) { acc += c.z; dd += 1; cnt = c.w; }
+        }
+      }
+      sm.rp[par][0] = dd;
+      sm.rp[par][1] = need - acc;
+      sm.rp[par][2] = cnt;
+    }
+  }
+  __syncthreads();
+  const Digit r{sm.rp[par][0], sm.rp[par][2]};
+  need = sm.rp[par][1];
+  return r;
+}
+
+// (a2) the n_below-th smallest (loss key, position) by radix select over the
+// 64-bit keys (digits constant over all losses skipped), then -- only when
+// several trials tie on that loss -- over the positions of the tied ones.
+__device__ Split compute_split(const FitArgs &A, const FitCtx &C, FitShared &sm) {
+  const int n = (int)A.n;
+  const int nb = A.n_below;
+  if (nb <= 0 || n == 0) return Split{0, 0, 0};
+  if (nb >= n) return Split{0, 0, 1};
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint64_t *lk = reinterpret_cast<uint64_t *>(C.lds + kOffKeys);
+  uint32_t *hist = reinterpret_cast<uint32_t *>(C.lds + kOffCnt);
+  uint64_t *keys = n <= kSortCap ? lk : C.gkeys;
+  for (int d = threadIdx.x; d < kDigits; d += blockDim.x) hist[d] = 0;
+  uint64_t an = ~0ull, on = 0ull;
+  for (int j = threadIdx.x; j < n; j += blockDim.x) {
+    const uint64_t k = sort_key(A.losses[j]);
+    keys[j] = k;
+    an &= k;
+    on |= k;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    an &= __shfl_xor(an, o, 64);
+    on |= __shfl_xor(on, o, 64);
+  }
+  if (lane == 0) { sm.vand[w] = an; sm.vor[w] = on; }
+  __syncthreads();
+  an = ~0ull;
+  on = 0ull;
+#pragma unroll
+  for (int i = 0; i < kFitWaves; ++i) { an &= sm.vand[i]; on |= sm.vor[i]; }
+  const uint64_t vary = an ^ on;
+  STAMP(11);
+  uint64_t mask = ~vary, prefix = an & ~vary;  // constant digits are known
+  uint32_t need = (uint32_t)nb, eq = (uint32_t)n;
+  int step = 0;
+  auto kv = [&](int j) { return keys[j]; };
+  for (int shift = 56; shift >= 0; shift -= 8) {
+    const uint64_t dm = 255ull << shift;
+    if ((vary & dm) == 0) continue;
+    const Digit g = select_digit(kv, n, mask, prefix, shift, need, hist + kDigits * (step & 1),
+                                 sm, step & 1);
+    ++step;
+    prefix |= (uint64_t)g.d << shift;
+    mask |= dm;
+    eq = g.cnt;
+    if (step <= 4) STAMP(11 + step);
+    // every key under this prefix is below: the largest key with the prefix
+    // is an exact threshold (usually after 2-3 digits)
+    if (need == eq) return Split{prefix | ~mask, ~0u, 2};
+  }
+  // prefix = threshold key T; `need` of the `eq` trials with key T are below
+  if (need == eq) return Split{prefix, ~0u, 2};
+  const uint64_t T = prefix;
+  uint64_t pmask = 0, pprefix = 0;
+  auto pv = [&](int j) { return keys[j] == T ? (uint64_t)j : ~0ull; };
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    const Digit g = select_digit(pv, n, pmask | 0xFFFFFFFF00000000ull, pprefix, shift, need,
+                                 hist + kDigits * (step & 1), sm, step & 1);
+    ++step;
+    pprefix |= (uint64_t)g.d << shift;
+    pmask |= 255ull << shift;
+  }
+  return Split{T, (uint32_t)pprefix, 2};
+}
+
+// ------------------------------------------------------------------------
+// per-component lpdf constants + truncation mass of one slot (block-wide);
+// w/mu/sg may be LDS or global; tmp: K doubles of scratch
+// ------------------------------------------------------------------------
+__device__ void prep_slot(const tpe_hp &H, int64_t slot, int K, const double *w, const double *mu,
+                          const double *sg, MixInfo *info, Coef *coef, int64_t kcap, double *tmp,
+                          FitShared &sm) {
+  Coef *cf = coef + slot * kcap;
+  const double wsum = block_np_sum(w, K, sm);
+  STAMP(7);
+  if (H.family == TPE_CAT) {
+    for (int k = threadIdx.x; k < K; k += blockDim.x) {
+      Coef c;
+      c.x = log(w[k]); c.y = 0.0; c.z = 0.0; c.w = 0.0;
+      cf[k] = c;
+    }
+    if (threadIdx.x == 0) {
+      MixInfo mi;
+      mi.K = K; mi.kind = 2; mi.p_accept = 1.0; mi.log_pacc = 0.0; mi.wsum = wsum;
+      info[slot] = mi;
+    }
+    return;
+  }
+  const bool bounded = (H.flags & (TPE_HAS_LOW | TPE_HAS_HIGH)) != 0;
+  double pacc = 1.0;
+  if (bounded) {  // tpe.py:130-136 / 273-276 (log-space bounds for LGMM)
+    for (int k = threadIdx.x; k < K; k += blockDim.x)
+      tmp[k] = w[k] * (normal_cdf(H.high, mu[k], sg[k]) - normal_cdf(H.low, mu[k], sg[k]));
+    __syncthreads();
+    pacc = block_np_sum(tmp, K, sm);
+  }
+  STAMP(8);
+  const bool quant = (H.flags & TPE_HAS_Q) != 0;
+  const double L2E = 1.4426950408889634;  // log2(e)
+  const double A0 = sqrt(0.5 * L2E);
+  for (int k = threadIdx.x; k < K; k += blockDim.x) {
+    Coef c;
+    const double s = sg[k];
+    const double sp = np_maximum(s, kEPS);
+    c.x = mu[k];
+    c.w = 0.0;
+    if (quant) {
+      c.y = 1.0 / np_maximum(1.4142135623730951 * s, kEPS);
+      c.z = w[k];
+    } else if (H.family == TPE_GMM) {
+      // log(w / sqrt(2 pi sigma^2) / p_accept), tpe.py:140-144
+      const double Z = sqrt(2.0 * 3.141592653589793 * (s * s));
+      c.y = A0 / sp;
+      c.z = L2E * log(w[k] / Z / pacc);
+    } else {
+      // lognormal_lpdf + log w, minus log(x) per candidate, tpe.py:193-202, 280
+      c.y = A0 / sp;
+      c.z = L2E * (log(w[k]) - log(sp * 2.5066282746310002));
+    }
+    cf[k] = c;
+  }
+  if (threadIdx.x == 0) {
+    MixInfo mi;
+    mi.K = K; mi.kind = quant ? 1 : 0; mi.p_accept = pacc; mi.log_pacc = log(pacc);
+    mi.wsum = wsum;
+    info[slot] = mi;
+  }
+}
+
+// ------------------------------------------------------------------------
+// (a4) adaptive_parzen_normal on the m observations ob[] (tid order) after
+// the sort; nlt = #{obs < prior_mu} = searchsorted(sorted, prior_mu, 'left')
+// ------------------------------------------------------------------------
+template <bool MIXLDS, typename PosT>
+__device__ void fit_continuous(const FitArgs &A, const FitCtx &C, FitShared &sm, const tpe_hp &H,
+                               int64_t slot, const double *ob, const PosT *perm, int m, int nlt) {
+  const double pm = H.prior_mu, ps = H.prior_sigma;
+  const int K = m + 1;
+  double *lm = reinterpret_cast<double *>(C.lds);
+  double *gw = A.mw + slot * A.kcap, *gm = A.mmu + slot * A.kcap, *gs = A.msig + slot * A.kcap;
+  double *mu = MIXLDS ? lm : gm;
+  double *w = MIXLDS ? lm + kMixStride : gw;
+  double *sg = MIXLDS ? lm + 2 * kMixStride : gs;
+  double *tmp = MIXLDS ? lm + 3 * kMixStride : A.tmp + slot * A.kcap;
+  int pos;
+  if (m == 0) pos = 0;                          // tpe.py:410-413
+  else if (m == 1) pos = (pm < ob[0]) ? 0 : 1;  // tpe.py:414-422
+  else pos = nlt;                               // tpe.py:427-428
+  const bool lfw = A.lf && A.lf < m;            // tpe.py:440
+  const LfRamp lr = lf_ramp(m, A.lf);
+  // place the sorted observations around the prior (tpe.py:429-432, 441-445)
+  if (MIXLDS) {
+    double v[4], wt[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = threadIdx.x + q * kFitThreads;
+      if (r < m) {
+        const int e = (int)perm[r];
+        v[q] = ob[e];
+        wt[q] = lfw ? lf_weight(lr, e) : 1.0;
+      }
+    }
+    __syncthreads();  // perm (LDS) is overwritten by the mixture arrays below
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = threadIdx.x + q * kFitThreads;
+      if (r < m) {
+        const int o = r + (r >= pos ? 1 : 0);
+        mu[o] = v[q];
+        w[o] = wt[q];
+      }
+    }
+  } else {
+    for (int r = threadIdx.x; r < m; r += blockDim.x) {
+      const int e = (int)perm[r];
+      const int o = r + (r >= pos ? 1 : 0);
+      mu[o] = ob[e];
+      w[o] = lfw ? lf_weight(lr, e) : 1.0;
+    }
+  }
+  if (threadIdx.x == 0) { mu[pos] = pm; w[pos] = A.prior_weight; }
+  __syncthreads();
+  STAMP(4);
+  // neighbour sigma (tpe.py:433-439), clip (456-460), prior sigma (461)
+  const double hi = ps / 1.0;
+  const double lo = ps / fmin(100.0, 1.0 + (double)K);
+  for (int k = threadIdx.x; k < K; k += blockDim.x) {
+    double s;
+    if (m == 0) s = ps;
+    else if (m == 1) s = (k == pos) ? ps : ps * .5;
+    else if (k == 0) s = mu[1] - mu[0];
+    else if (k == K - 1) s = mu[K - 1] - mu[K - 2];
+    else s = np_maximum(mu[k] - mu[k - 1], mu[k + 1] - mu[k]);
+    s = np_minimum(np_maximum(s, lo), hi);
+    if (k == pos) s = ps;
+    sg[k] = s;
+  }
+  STAMP(5);
+  const double tot = block_np_sum(w, K, sm);  // tpe.py:468 (its barriers cover sg too)
+  // normalise, and the truncation-mass terms of the same component
+  // (tpe.py:130-136 / 273-276; LGMM bounds are log-space) -- no barrier between
+  const bool bounded = (H.flags & (TPE_HAS_LOW | TPE_HAS_HIGH)) != 0;
+  for (int k = threadIdx.x; k < K; k += blockDim.x) {
+    const double wk = w[k] / tot;
+    w[k] = wk;
+    if (bounded)
+      tmp[k] = wk * (normal_cdf(H.high, mu[k], sg[k]) - normal_cdf(H.low, mu[k], sg[k]));
+  }
+  STAMP(6);
+  double sums[2];
+  {
+    const double *const arr[2] = {w, tmp};
+    if (bounded) block_np_sums<2>(arr, K, sm, sums);
+    else { const double *const a1[1] = {w}; double s1[1]; block_np_sums<1>(a1, K, sm, s1); sums[0] = s1[0]; sums[1] = 1.0; }
+  }
+  STAMP(8);
+  const double wsum = sums[0], pacc = sums[1];
+  // per-component lpdf constants (tpe.py:138-160, 277-299) + copy-out
+  const bool quant = (H.flags & TPE_HAS_Q) != 0;
+  const double L2E = 1.4426950408889634;  // log2(e)
+  const double A0 = sqrt(0.5 * L2E);
+  Coef *cf = A.coef + slot * A.kcap;
+  for (int k = threadIdx.x; k < K; k += blockDim.x) {
+    const double s = sg[k], wk = w[k], mk = mu[k];
+    const double sp = np_maximum(s, kEPS);
+    Coef c;
+    c.x = mk;
+    c.w = 0.0;
+    if (quant) {
+      c.y = 1.0 / np_maximum(1.4142135623730951 * s, kEPS);
+      c.z = wk;
+    } else if (H.family == TPE_GMM) {
+      // log(w / sqrt(2 pi sigma^2) / p_accept), tpe.py:140-144
+      const double Z = sqrt(2.0 * 3.141592653589793 * (s * s));
+      c.y = A0 / sp;
+      c.z = L2E * log(wk / Z / pacc);
+    } else {
+      // lognormal_lpdf + log w, minus log(x) per candidate, tpe.py:193-202, 280
+      c.y = A0 / sp;
+      c.z = L2E * (log(wk) - log(sp * 2.5066282746310002));
+    }
+    cf[k] = c;
+    if (MIXLDS) { gw[k] = wk; gm[k] = mk; gs[k] = s; }
+  }
+  if (threadIdx.x == 0) {
+    MixInfo mi;
+    mi.K = K; mi.kind = quant ? 1 : 0; mi.p_accept = pacc; mi.log_pacc = log(pacc);
+    mi.wsum = wsum;
+    A.info[slot] = mi;
+  }
+}
+
+// ------------------------------------------------------------------------
+// (a8) categorical posterior: LF-weighted bincount in observation order
+// (np.bincount adds sequentially per bin), + pseudocounts, normalised.
+// perm: observations stably sorted by category -> one segment per bin whose
+// serial sum keeps the reference's rounding.
+// ------------------------------------------------------------------------
+template <typename PosT>
+__device__ void fit_categorical(const FitArgs &A, const FitCtx &C, FitShared &sm,
+                                const tpe_hp &H, int64_t slot, const uint64_t *keys,
+                                const PosT *perm, int m) {
+  const int upper = H.upper;
+  double *w = A.mw + slot * A.kcap, *mu = A.mmu + slot * A.kcap, *sg = A.msig + slot * A.kcap;
+  // segment bounds per bin: LDS (cnt/run region) when they fit, else the
+  // (not yet written) global mu array of the slot
+  int *seg = upper <= 4096 ? reinterpret_cast<int *>(C.lds + kOffCnt) : reinterpret_cast<int *>(mu);
+  for (int c = threadIdx.x; c < 2 * upper; c += blockDim.x) seg[c] = 0;
+  __syncthreads();
+  for (int r = threadIdx.x; r < m; r += blockDim.x) {
+    const uint64_t b = keys[perm[r]];
+    if (b >= (uint64_t)upper) continue;
+    if (r == 0 || keys[perm[r - 1]] != b) seg[2 * b] = r;
+    if (r == m - 1 || keys[perm[r + 1]] != b) seg[2 * b + 1] = r + 1;
+  }
+  __syncthreads();  // keys are dead from here on
+  // LF weights in sorted order, in parallel (LDS over the keys, or HBM scratch)
+  double *ws = m <= kSortCap ? reinterpret_cast<double *>(C.lds + kOffKeys) : A.ob + slot * A.kcap;
+  const LfRamp lr = lf_ramp(m, A.lf);
+  for (int r = threadIdx.x; r < m; r += blockDim.x) ws[r] = lf_weight(lr, (int64_t)perm[r]);
+  __syncthreads();
+  for (int c = threadIdx.x; c < upper; c += blockDim.x) {
+    // serial per bin (np.bincount order); loads run 8 ahead of the adds
+    double cnt = 0.0;
+    const int r1 = seg[2 * c + 1];
+    int r = seg[2 * c];
+    for (; r + 8 <= r1; r += 8) {
+      double wv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) wv[u] = ws[r + u];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) cnt += wv[u];
+    }
+    for (; r < r1; ++r) cnt += ws[r];
+    double pc;
+    if (H.flags & TPE_PCHOICE)
+      pc = cnt + (double)upper * (A.prior_weight * A.pprior[H.pprior_begin + c]);
+    else
+      pc = cnt + A.prior_weight;
+    w[c] = pc;
+  }
+  __syncthreads();
+  STAMP(5);
+  const double tot = block_np_sum(w, upper, sm);
+  for (int c = threadIdx.x; c < upper; c += blockDim.x) {
+    w[c] = w[c] / tot;
+    mu[c] = 0.0;
+    sg[c] = 0.0;
+  }
+  __syncthreads();
+  prep_slot(H, slot, upper, w, mu, sg, A.info, A.coef, A.kcap, A.tmp + slot * A.kcap, sm);
+}
+
+// ------------------------------------------------------------------------
+// k_fit: split + fit + lpdf constants, one block per (hp, side)
+// ------------------------------------------------------------------------
+__global__ __launch_bounds__(kFitThreads) void k_fit(FitArgs A) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char dyn_lds[];
+  __shared__ FitShared sm;
+  const int hp = blockIdx.x, side = blockIdx.y;  // side 0 = below ("good")
+  const int64_t slot = 2 * (int64_t)hp + side;
+  const tpe_hp H = A.hps[hp];
+  if (threadIdx.x == 0) sm.np.n = -1;
+  FitCtx C;
+  C.lds = dyn_lds;
+  unsigned char *gsb = A.sortbuf + slot * 16 * A.scap;
+  C.gkeys = reinterpret_cast<uint64_t *>(gsb);
+  C.gpa = reinterpret_cast<uint32_t *>(gsb + 8 * A.scap);
+  C.gpb = C.gpa + A.scap;
+  STAMP(0);
+  const Split t = compute_split(A, C, sm);
+  __syncthreads();
+  STAMP(1);
+
+  // ---- gather this side's observations in tid order (tpe.py:629-636):
+  // 4 consecutive trials per thread, one block scan per 4096 trials
+  const bool cat = H.family == TPE_CAT;
+  const double *row = A.vals + (int64_t)hp * A.n;
+  const uint8_t *arow = A.active + (int64_t)hp * A.n;
+  double *ob = A.ob + slot * A.kcap;
+  uint64_t *lk = reinterpret_cast<uint64_t *>(dyn_lds + kOffKeys);
+  int m = 0, nlt = 0;
+  for (int64_t c0 = 0; c0 < A.n; c0 += 4 * kFitThreads) {
+    const int64_t j0 = c0 + 4 * (int64_t)threadIdx.x;
+    bool f[4];
+    double v[4];
+    int cntl = 0;
+    // all loads issued before any use: one memory round trip per chunk
+    uint8_t ac[4];
+    double ls[4], rv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t j = min<int64_t>(j0 + u, A.n - 1);
+      ac[u] = arow[j];
+      ls[u] = A.losses[j];
+      rv[u] = row[j];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t j = j0 + u;
+      f[u] = j < A.n && ac[u] && (is_below(t, sort_key(ls[u]), (uint32_t)j) == (side == 0));
+      v[u] = 0.0;
+      if (f[u]) {
+        v[u] = obs_transform(rv[u], H.obs_transform, H.low);
+        nlt += (v[u] < H.prior_mu) ? 1 : 0;
+      }
+      cntl += f[u] ? 1 : 0;
+    }
+    int tot;
+    int i = m + block_excl_scan(cntl, sm.wsum, tot);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (!f[u]) continue;
+      ob[i] = v[u];
+      const uint64_t k = cat ? (uint64_t)(int64_t)v[u] : sort_key(v[u]);
+      if (i < kSortCap) lk[i] = k;
+      else C.gkeys[i] = k;
+      ++i;
+    }
+    m += tot;
+  }
+  nlt = block_sum_int(nlt, sm.isum);
+  const bool lds_sort = m <= kSortCap;
+  if (!lds_sort)
+    for (int i = threadIdx.x; i < kSortCap; i += blockDim.x) C.gkeys[i] = lk[i];
+  __syncthreads();
+  STAMP(2);
+
+  uint32_t *cnt = reinterpret_cast<uint32_t *>(dyn_lds + kOffCnt);
+  uint32_t *run = reinterpret_cast<uint32_t *>(dyn_lds + kOffRun);
+  if (lds_sort) {
+    const uint16_t *perm = block_sort_perm<uint16_t>(
+        lk, reinterpret_cast<uint16_t *>(dyn_lds + kOffPosA),
+        reinterpret_cast<uint16_t *>(dyn_lds + kOffPosB), m, cnt, run, sm);
+    STAMP(3);
+    if (cat) fit_categorical<uint16_t>(A, C, sm, H, slot, lk, perm, m);
+    else if (m + 1 <= kMixLds) fit_continuous<true, uint16_t>(A, C, sm, H, slot, ob, perm, m, nlt);
+    else fit_continuous<false, uint16_t>(A, C, sm, H, slot, ob, perm, m, nlt);
+  } else {
+    const uint32_t *perm = block_sort_perm<uint32_t>(C.gkeys, C.gpa, C.gpb, m, cnt, run, sm);
+    STAMP(3);
+    if (cat) fit_categorical<uint32_t>(A, C, sm, H, slot, C.gkeys, perm, m);
+    else fit_continuous<false, uint32_t>(A, C, sm, H, slot, ob, perm, m, nlt);
+  }
+  __syncthreads();
+  STAMP(10);
+}
+
+// operator-level split (tpe_split): same threshold, then the mask
+__global__ __launch_bounds__(kFitThreads) void k_split(FitArgs A, uint8_t *__restrict__ below) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char dyn_lds[];
+  __shared__ FitShared sm;
+  if (threadIdx.x == 0) sm.np.n = -1;
+  FitCtx C;
+  C.lds = dyn_lds;
+  C.gkeys = reinterpret_cast<uint64_t *>(A.sortbuf);
+  C.gpa = reinterpret_cast<uint32_t *>(A.sortbuf + 8 * A.scap);
+  C.gpb = C.gpa + A.scap;
+  const Split t = compute_split(A, C, sm);
+  for (int64_t j = threadIdx.x; j < A.n; j += blockDim.x)
+    below[j] = is_below(t, sort_key(A.losses[j]), (uint32_t)j) ? 1 : 0;
+}
+
+// constants of explicitly given mixtures (operator-level tpe_score/lpdf)
+__global__ __launch_bounds__(256) void k_prep(const tpe_hp *__restrict__ hps,
+                                              const double *__restrict__ mw,
+                                              const double *__restrict__ mmu,
+                                              const double *__restrict__ msig,
+                                              MixInfo *__restrict__ info, Coef *__restrict__ coef,
+                                              int64_t kcap, double *__restrict__ scratch) {
+  __shared__ FitShared sm;
+  if (threadIdx.x == 0) sm.np.n = -1;
+  const int hp = blockIdx.x, side = blockIdx.y;
+  const int64_t slot = 2 * (int64_t)hp + side;
+  const tpe_hp H = hps[hp];
+  const int K = info[slot].K;
+  __syncthreads();
+  prep_slot(H, slot, K, mw + slot * kcap, mmu + slot * kcap, msig + slot * kcap, info, coef, kcap,
+            scratch + slot * kcap, sm);
+}
+
+// ------------------------------------------------------------------------
+#ifdef TPE_STAMPS
+}  // namespace tpe
+extern "C" int tpe_debug_stamps(unsigned long long *out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(tpe::g_stamps), sizeof(tpe::g_stamps)) == hipSuccess
+             ? 0 : -5;
+}
+namespace tpe {
+#endif
+
+hipError_t launch_fit(const FitArgs &a, int32_t n_hp, hipStream_t st) {
+  if (n_hp <= 0) return hipSuccess;
+  k_fit<<<dim3(n_hp, 2), kFitThreads, kFitLds, st>>>(a);
+  return hipGetLastError();
+}
+
+hipError_t launch_split(const FitArgs &a, uint8_t *below, hipStream_t st) {
+  k_split<<<1, kFitThreads, kFitLds, st>>>(a, below);
+  return hipGetLastError();
+}
+
+hipError_t launch_prep(const tpe_hp *hps, int32_t n_hp, const double *mw, const double *mmu,
+                       const double *msig, MixInfo *info, Coef *coef, int64_t kcap,
+                       double *scratch, hipStream_t st) {
+  if (n_hp <= 0) return hipSuccess;
+  k_prep<<<dim3(n_hp, 2), 256, 0, st>>>(hps, mw, mmu, msig, info, coef, kcap, scratch);
+  return hipGetLastError();
+}
+
+}  // namespace tpe

@@ -83,15 +83,30 @@ struct ScoreArgs {
   int32_t accumulate;        // merge with results of an earlier candidate chunk
 };
 
-// ---- launch wrappers (tpe_kernels.hip) ----
-hipError_t launch_split(const double *losses, int64_t n, int32_t n_below,
-                        uint8_t *below, hipStream_t st);
-hipError_t launch_fit(const tpe_hp *hps, int32_t n_hp, const double *vals,
-                      const uint8_t *active, const double *losses, int64_t n,
-                      int32_t n_below, double prior_weight, int32_t lf,
-                      const double *pprior, double *mw, double *mmu, double *msig,
-                      MixInfo *info, Coef *coef, int64_t kcap, double *scratch,
-                      double *scratch2, hipStream_t st);
+// Arguments of the fit kernels (tpe_fit.hip), one block per (hp, side) slot.
+struct FitArgs {
+  const tpe_hp *hps;
+  const double *vals;        // [P][n] history values (tid order)
+  const uint8_t *active;     // [P][n]
+  const double *losses;      // [n]
+  int64_t n;
+  int32_t n_below;
+  int32_t lf;
+  double prior_weight;
+  const double *pprior;
+  double *mw, *mmu, *msig;   // [2P][kcap] fitted mixtures
+  MixInfo *info;             // [2P]
+  Coef *coef;                // [2P][kcap]
+  int64_t kcap;
+  double *ob;                // [2P][kcap] scratch: observations of the slot
+  double *tmp;               // [2P][kcap] scratch (may alias ob)
+  unsigned char *sortbuf;    // [2P][16 * scap] global sort keys + permutations
+  int64_t scap;              // >= n
+};
+
+// ---- launch wrappers (tpe_fit.hip / tpe_kernels.hip) ----
+hipError_t launch_split(const FitArgs &a, uint8_t *below, hipStream_t st);
+hipError_t launch_fit(const FitArgs &a, int32_t n_hp, hipStream_t st);
 hipError_t launch_prep(const tpe_hp *hps, int32_t n_hp, const double *mw,
                        const double *mmu, const double *msig, MixInfo *info,
                        Coef *coef, int64_t kcap, double *scratch,

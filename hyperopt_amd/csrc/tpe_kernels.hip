@@ -1,11 +1,8 @@
 // tpe_kernels.hip -- hand-written CDNA4 (gfx950) kernels of the TPE hot path.
 //
-// Reference semantics (pminervini/hyperopt, hyperopt/tpe.py):
-//   k_split   : ap_filter_trials loss ranking            tpe.py:613-641
-//   k_fit     : adaptive_parzen_normal / categorical      tpe.py:381-475, 573-607
-//   k_prep    : GMM1_lpdf / LGMM1_lpdf per-component      tpe.py:104-166, 259-301
-//               constants, truncation mass p_accept
-//   k_score   : candidate draw (GMM1/LGMM1/categorical,   tpe.py:62-93, 216-250
+// Reference semantics (pminervini/hyperopt, hyperopt/tpe.py); the split and
+// the Parzen fits are in tpe_fit.hip.
+//   k_draw   : candidate draw (GMM1/LGMM1/categorical,   tpe.py:62-93, 216-250
 //               counter-based Philox in registers), below/above lpdf
 //               (log-sum-exp or linear erf-CDF sum), EI and block argmax
 //                                                         tpe.py:684-698, 749-759
@@ -18,625 +15,11 @@
 
 #include <algorithm>
 
-#include "tpe_internal.hpp"
+#include "tpe_device.hpp"
 
 namespace tpe {
 
-#ifdef TPE_STAMPS
-// debug build only: per-block phase timestamps of k_fit (wall clock, 100 MHz)
-__device__ unsigned long long g_stamps[512][16];
-#define STAMP(slot, ph) do { if (threadIdx.x == 0) g_stamps[(slot) & 511][ph] = wall_clock64(); } while (0)
-#else
-#define STAMP(slot, ph) do {} while (0)
-#endif
-
-// ------------------------------------------------------------------------
-// numpy-compatible scalar helpers
-// ------------------------------------------------------------------------
-__device__ __forceinline__ double np_maximum(double a, double b) {
-  if (a != a) return a;
-  if (b != b) return b;
-  return a >= b ? a : b;
-}
-__device__ __forceinline__ double np_minimum(double a, double b) {
-  if (a != a) return a;
-  if (b != b) return b;
-  return a <= b ? a : b;
-}
-
-// numpy float64 sum (np.sum / ndarray.sum): the reduction runs over buffers
-// of 8192 elements; each buffer is summed by numpy's pairwise_sum (blocks of
-// <= 128 with 8 accumulators, split at n/2 rounded down to a multiple of 8).
-// Reproducing it keeps the Parzen weights and p_accept bit-identical.
-__device__ double np_leaf_sum(const double *a, int n) {
-#pragma clang fp contract(off)
-  if (n < 8) {
-    double r = 0.0;
-    for (int i = 0; i < n; ++i) r += a[i];
-    return r;
-  }
-  double r0 = a[0], r1 = a[1], r2 = a[2], r3 = a[3], r4 = a[4], r5 = a[5],
-         r6 = a[6], r7 = a[7];
-  int i = 8;
-  for (; i < n - (n % 8); i += 8) {
-    r0 += a[i + 0]; r1 += a[i + 1]; r2 += a[i + 2]; r3 += a[i + 3];
-    r4 += a[i + 4]; r5 += a[i + 5]; r6 += a[i + 6]; r7 += a[i + 7];
-  }
-  double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-  for (; i < n; ++i) res += a[i];
-  return res;
-}
-
-template <int D>
-__device__ void np_leaves(int off, int n, int *lo, int *ln, int &cnt) {
-  if (n <= 128) { lo[cnt] = off; ln[cnt] = n; ++cnt; return; }
-  int n2 = n / 2;
-  n2 -= n2 % 8;
-  np_leaves<D - 1>(off, n2, lo, ln, cnt);
-  np_leaves<D - 1>(off + n2, n - n2, lo, ln, cnt);
-}
-template <>
-__device__ void np_leaves<0>(int off, int n, int *lo, int *ln, int &cnt) {
-  lo[cnt] = off; ln[cnt] = n; ++cnt;
-}
-template <int D>
-__device__ double np_combine(int n, const double *leaf, int &idx) {
-  if (n <= 128) return leaf[idx++];
-  int n2 = n / 2;
-  n2 -= n2 % 8;
-  const double a = np_combine<D - 1>(n2, leaf, idx);
-  const double b = np_combine<D - 1>(n - n2, leaf, idx);
-  return a + b;
-}
-template <>
-__device__ double np_combine<0>(int n, const double *leaf, int &idx) {
-  return leaf[idx++];
-}
-
-// Block-cooperative np.sum of a[0..n) (a in global memory, written by this
-// block before the call and visible after __syncthreads()).
-struct NpSumSmem {
-  int lo[kMaxLeaves];
-  int ln[kMaxLeaves];
-  double leaf[kMaxLeaves];
-  int cnt;
-  double total;
-};
-__device__ double block_np_sum(const double *a, int64_t n, NpSumSmem &sm) {
-#pragma clang fp contract(off)
-  double total = 0.0;
-  for (int64_t c0 = 0; c0 < n; c0 += 8192) {
-    const int cn = (int)min<int64_t>(8192, n - c0);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      int cnt = 0;
-      np_leaves<8>(0, cn, sm.lo, sm.ln, cnt);
-      sm.cnt = cnt;
-    }
-    __syncthreads();
-    for (int l = threadIdx.x; l < sm.cnt; l += blockDim.x)
-      sm.leaf[l] = np_leaf_sum(a + c0 + sm.lo[l], sm.ln[l]);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      int idx = 0;
-      const double part = np_combine<8>(cn, sm.leaf, idx);
-      sm.total = (c0 == 0) ? (0.0 + part) : (sm.total + part);
-    }
-  }
-  __syncthreads();
-  if (n > 0) total = sm.total;
-  __syncthreads();
-  return total;
-}
-
-// Block-wide exclusive scan of small ints (blockDim multiple of 64).
-__device__ int block_excl_scan(int v, int *wsum, int &total) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int nw = blockDim.x >> 6;
-  int x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) wsum[wid] = x;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int acc = 0;
-    for (int w = 0; w < nw; ++w) {
-      const int t = wsum[w];
-      wsum[w] = acc;
-      acc += t;
-    }
-    wsum[nw] = acc;
-  }
-  __syncthreads();
-  const int res = wsum[wid] + x - v;
-  total = wsum[nw];
-  __syncthreads();
-  return res;
-}
-
-template <typename T>
-__device__ T block_sum_i(T v, T *buf) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  if (lane == 0) buf[wid] = v;
-  __syncthreads();
-  T t = 0;
-  if (threadIdx.x == 0) {
-    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += buf[w];
-    buf[0] = t;
-  }
-  __syncthreads();
-  t = buf[0];
-  __syncthreads();
-  return t;
-}
-
-// ------------------------------------------------------------------------
-// Block-wide bitonic sort of (key, position) pairs in LDS, ascending in the
-// total order "numpy argsort with NaN last, ties by position" (stable).
-// np2 = power of two >= n; slots [n, np2) are padded with (NaN, INT_MAX).
-// ------------------------------------------------------------------------
-constexpr int kSortMax = 8192;  // 8192 x (8 + 4) B = 96 KB of LDS
-
-__device__ __forceinline__ bool key_less(double a, int64_t ia, double b, int64_t ib);
-
-__device__ void block_bitonic_sort(double *key, int *pos, int n, int np2) {
-  for (int i = n + threadIdx.x; i < np2; i += blockDim.x) {
-    key[i] = NAN;
-    pos[i] = 0x7fffffff;
-  }
-  __syncthreads();
-  for (int k = 2; k <= np2; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int t = threadIdx.x; t < (np2 >> 1); t += blockDim.x) {
-        const int i = 2 * t - (t & (j - 1));
-        const int l = i + j;
-        const bool up = (i & k) == 0;
-        const double ki = key[i], kl = key[l];
-        const int pi = pos[i], pl = pos[l];
-        if (key_less(kl, pl, ki, pi) == up) {
-          key[i] = kl; key[l] = ki;
-          pos[i] = pl; pos[l] = pi;
-        }
-      }
-      __syncthreads();
-    }
-  }
-}
-
-__device__ __forceinline__ int pow2_at_least(int n) {
-  int p = 2;
-  while (p < n) p <<= 1;
-  return p;
-}
-
-// ------------------------------------------------------------------------
-// (a2) split: mark the n_below lowest losses.  Key order = numpy argsort with
-// NaN last; ties by position (stable).  One block, n_below <= 25 rounds of a
-// block-wide argmin (top-k with k <= 25).
-// ------------------------------------------------------------------------
-__device__ __forceinline__ bool key_less(double a, int64_t ia, double b,
-                                         int64_t ib) {
-  const bool na = a != a, nb = b != b;
-  if (na != nb) return nb;  // non-NaN before NaN
-  if (!na && a != b) return a < b;
-  return ia < ib;
-}
-
-__global__ __launch_bounds__(1024) void k_split(const double *__restrict__ losses,
-                                                int64_t n, int32_t n_below,
-                                                uint8_t *__restrict__ below) {
-  extern __shared__ __attribute__((aligned(16))) double dyn_lds[];
-  __shared__ double sv[16];
-  __shared__ int64_t si[16];
-  for (int64_t j = threadIdx.x; j < n; j += blockDim.x) below[j] = 0;
-  __syncthreads();
-  if (n <= kSortMax) {  // one LDS sort, then the first n_below are "good"
-    double *key = dyn_lds;
-    int *pos = reinterpret_cast<int *>(dyn_lds + kSortMax);
-    for (int i = threadIdx.x; i < n; i += blockDim.x) { key[i] = losses[i]; pos[i] = i; }
-    __syncthreads();
-    block_bitonic_sort(key, pos, (int)n, pow2_at_least((int)n));
-    for (int r = threadIdx.x; r < n_below && r < n; r += blockDim.x) below[pos[r]] = 1;
-    return;
-  }
-  // previous winner (strict lower bound of remaining keys)
-  double pv = -INFINITY;
-  int64_t pi = -1;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  for (int r = 0; r < n_below && r < n; ++r) {
-    double bv = NAN;
-    int64_t bi = -1;
-    for (int64_t j = threadIdx.x; j < n; j += blockDim.x) {
-      const double v = losses[j];
-      if (pi >= 0 && !key_less(pv, pi, v, j)) continue;  // already taken
-      if (bi < 0 || key_less(v, j, bv, bi)) { bv = v; bi = j; }
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const double ov = __shfl_xor(bv, o, 64);
-      const int64_t oi = __shfl_xor(bi, o, 64);
-      if (oi >= 0 && (bi < 0 || key_less(ov, oi, bv, bi))) { bv = ov; bi = oi; }
-    }
-    if (lane == 0) { sv[wid] = bv; si[wid] = bi; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      for (int w = 1; w < (int)(blockDim.x >> 6); ++w)
-        if (si[w] >= 0 && (bi < 0 || key_less(sv[w], si[w], bv, bi))) {
-          bv = sv[w]; bi = si[w];
-        }
-      sv[0] = bv; si[0] = bi;
-      if (bi >= 0) below[bi] = 1;
-    }
-    __syncthreads();
-    pv = sv[0]; pi = si[0];
-    __syncthreads();
-  }
-}
-
-// ------------------------------------------------------------------------
-// (a3)/(a4)/(a8) Parzen fit / categorical posterior, one block per (hp, side)
-// ------------------------------------------------------------------------
-// linear_forgetting_weights(n, lf)[i], tpe.py:381-394, with numpy linspace
-// rounding (i*step + start; last element == stop).
-__device__ __forceinline__ double lf_weight(int64_t i, int64_t n, int32_t lf) {
-#pragma clang fp contract(off)
-  if (n < lf) return 1.0;
-  const int64_t m = n - lf;  // ramp length
-  if (i >= m) return 1.0;
-  const double start = 1.0 / (double)n;
-  if (m == 1) return start;
-  if (i == m - 1) return 1.0;
-  const double step = (1.0 - start) / (double)(m - 1);
-  return (double)i * step + start;
-}
-
-__device__ __forceinline__ double obs_transform(double v, int32_t tf, double low) {
-  switch (tf) {
-    case TPE_OBS_LOG: return log(v);
-    case TPE_OBS_LOG_CLIP_EXPLOW: return log(np_maximum(v, np_maximum(kEPS, exp(low))));
-    case TPE_OBS_LOG_CLIP_EPS: return log(np_maximum(v, kEPS));
-    default: return v;
-  }
-}
-
-// rank of element i in a stable ascending sort with NaN last
-__device__ __forceinline__ bool before(double vj, int64_t j, double vi, int64_t i) {
-  if (vi != vi) return (vj == vj) || j < i;
-  return vj < vi || (vj == vi && j < i);
-}
-
-struct FitSmem {
-  int wsum[17];
-  int64_t cnt64[16];
-  NpSumSmem np;
-};
-
-__device__ void prep_slot(const tpe_hp &H, int64_t slot, const double *w, const double *mu,
-                          const double *sg, MixInfo *info, Coef *coef, int64_t kcap,
-                          double *scratch, NpSumSmem &np);
-
-// The n_below-th smallest loss key (value, position) in numpy argsort order
-// (NaN last, ties by position): one wave, n_below <= 25 rounds of a wave-wide
-// argmin over the keys above the previous winner -- no block barriers.
-// below(j) <=> key(j) <= threshold.  n_below == 0 -> position -1 (none).
-__device__ void split_threshold(const double *__restrict__ losses, int64_t n, int32_t n_below,
-                                double &tv, int64_t &ti) {
-  double pv = -INFINITY;
-  int64_t pi = -1;
-  const int lane = threadIdx.x & 63;
-  for (int r = 0; r < n_below && r < n; ++r) {
-    double bv = NAN;
-    int64_t bi = -1;
-    for (int64_t j = lane; j < n; j += 64) {
-      const double v = losses[j];
-      if (pi >= 0 && !key_less(pv, pi, v, j)) continue;
-      if (bi < 0 || key_less(v, j, bv, bi)) { bv = v; bi = j; }
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const double ov = __shfl_xor(bv, o, 64);
-      const int64_t oi = __shfl_xor(bi, o, 64);
-      if (oi >= 0 && (bi < 0 || key_less(ov, oi, bv, bi))) { bv = ov; bi = oi; }
-    }
-    pv = bv;
-    pi = bi;
-  }
-  tv = pv;
-  ti = pi;
-}
-
-// Split + Parzen fit (or categorical posterior) + lpdf constants of one
-// (hp, side) slot, one 1024-thread block each: tpe.py:613-641, 381-475,
-// 573-607, 104-166, 259-301 in a single launch.
-__global__ __launch_bounds__(1024) void k_fit(
-    const tpe_hp *__restrict__ hps, const double *__restrict__ vals,
-    const uint8_t *__restrict__ active, const double *__restrict__ losses,
-    int64_t n, int32_t n_below, double prior_weight, int32_t lf,
-    const double *__restrict__ pprior,
-    double *__restrict__ mw, double *__restrict__ mmu, double *__restrict__ msig,
-    MixInfo *__restrict__ info, Coef *__restrict__ coef, int64_t kcap,
-    double *__restrict__ scratch, double *__restrict__ scratch2) {
-#pragma clang fp contract(off)
-  extern __shared__ __attribute__((aligned(16))) double dyn_lds[];
-  __shared__ FitSmem sm;
-  __shared__ double thr_v;
-  __shared__ int64_t thr_i;
-  const int hp = blockIdx.x, side = blockIdx.y;  // side 0 = below ("good")
-  const int64_t slot = 2 * (int64_t)hp + side;
-  const tpe_hp H = hps[hp];
-  double *w = mw + slot * kcap;
-  double *mu = mmu + slot * kcap;
-  double *sg = msig + slot * kcap;
-  double *ob = scratch + slot * kcap;  // observations in tid order
-  const double *row = vals + (int64_t)hp * n;
-  const uint8_t *arow = active + (int64_t)hp * n;
-  STAMP(slot, 0);
-  // ---- good/bad split: threshold key of the n_below best losses
-  if (threadIdx.x < 64) {
-    double tv;
-    int64_t ti;
-    split_threshold(losses, n, n_below, tv, ti);
-    if (threadIdx.x == 0) { thr_v = tv; thr_i = ti; }
-  }
-  __syncthreads();
-  const double tv = thr_v;
-  const int64_t ti = thr_i;
-  STAMP(slot, 1);
-
-  // ---- gather this side's observations, keeping tid order (tpe.py:629-636)
-  int m = 0;
-  for (int64_t c0 = 0; c0 < n; c0 += blockDim.x) {
-    const int64_t j = c0 + threadIdx.x;
-    bool f = j < n && arow[j];
-    if (f) {
-      const bool good = ti >= 0 && !key_less(tv, ti, losses[j], j);   // key(j) <= thr
-      f = good == (side == 0);
-    }
-    int tot;
-    const int pos = block_excl_scan(f ? 1 : 0, sm.wsum, tot);
-    if (f) ob[m + pos] = obs_transform(row[j], H.obs_transform, H.low);
-    m += tot;
-  }
-  __syncthreads();
-  STAMP(slot, 2);
-  // LDS layout (96 KB): m <= kSortMax -> key[8192] f64 + pos[8192] i32;
-  // otherwise an LDS copy of the observations when <= 12288 of them fit.
-  const bool small = m <= kSortMax;
-  double *sob = dyn_lds;
-  int *spos = reinterpret_cast<int *>(dyn_lds + kSortMax);
-  if (m <= 12288) {
-    for (int i = threadIdx.x; i < m; i += blockDim.x) sob[i] = ob[i];
-    __syncthreads();
-  } else {
-    sob = ob;
-  }
-  STAMP(slot, 3);
-
-  if (H.family == TPE_CAT) {
-    // LF-weighted bincount in observation order (np.bincount) + pseudocounts.
-    // Weights precomputed in parallel (LDS) so each bin's serial sum -- kept
-    // serial for bit-identical rounding -- is a short dependent chain.
-    const int upper = H.upper;
-    if (small) {
-      for (int i = threadIdx.x; i < m; i += blockDim.x) {
-        spos[i] = (int)sob[i];
-        sob[i] = lf_weight(i, m, lf);
-      }
-      __syncthreads();
-    }
-    for (int c = threadIdx.x; c < upper; c += blockDim.x) {
-      double cnt = 0.0;
-      if (small) {
-        for (int i = 0; i < m; ++i)
-          if (spos[i] == c) cnt += sob[i];
-      } else {
-        for (int i = 0; i < m; ++i)
-          if ((int64_t)sob[i] == c) cnt += lf_weight(i, m, lf);
-      }
-      double pc;
-      if (H.flags & TPE_PCHOICE)
-        pc = cnt + (double)upper * (prior_weight * pprior[H.pprior_begin + c]);
-      else
-        pc = cnt + prior_weight;
-      w[c] = pc;
-    }
-    __syncthreads();
-    STAMP(slot, 4);
-    const double tot = block_np_sum(w, upper, sm.np);
-    for (int c = threadIdx.x; c < upper; c += blockDim.x) {
-      w[c] = w[c] / tot;
-      mu[c] = 0.0;
-      sg[c] = 0.0;
-    }
-    if (threadIdx.x == 0) { info[slot].K = upper; info[slot].kind = 2; }
-    __syncthreads();
-    prep_slot(H, slot, w, mu, sg, info, coef, kcap, scratch2, sm.np);
-    __syncthreads();
-    STAMP(slot, 10);
-    return;
-  }
-
-  const double pm = H.prior_mu, ps = H.prior_sigma;
-  int pos = 0;
-  if (m == 0) {  // tpe.py:410-413
-    if (threadIdx.x == 0) { mu[0] = pm; sg[0] = ps; w[0] = prior_weight; }
-  } else if (m == 1) {  // tpe.py:414-422
-    if (threadIdx.x == 0) {
-      const double o = sob[0];
-      if (pm < o) {
-        pos = 0; mu[0] = pm; mu[1] = o; sg[0] = ps; sg[1] = ps * .5;
-      } else {
-        pos = 1; mu[0] = o; mu[1] = pm; sg[0] = ps * .5; sg[1] = ps;
-      }
-      w[0] = 1.0; w[1] = 1.0; w[pos] = prior_weight;
-    }
-  } else {  // tpe.py:423-454
-    // prior_pos = searchsorted(sorted, prior_mu, 'left') = #{obs < pm}
-    int cl = 0;
-    for (int i = threadIdx.x; i < m; i += blockDim.x) cl += (sob[i] < pm) ? 1 : 0;
-    pos = block_sum_i<int>(cl, sm.wsum);
-    const bool lfw = lf && lf < m;
-    if (small) {
-      // stable LDS bitonic sort; sorted slot r goes to r + (r >= prior_pos)
-      for (int i = threadIdx.x; i < m; i += blockDim.x) spos[i] = i;
-      __syncthreads();
-      block_bitonic_sort(sob, spos, m, pow2_at_least(m));
-      for (int r = threadIdx.x; r < m; r += blockDim.x) {
-        const int o = r + (r >= pos ? 1 : 0);
-        mu[o] = sob[r];
-        w[o] = lfw ? lf_weight(spos[r], m, lf) : 1.0;
-      }
-    }
-    // large m: rank by counting (stable; 4 elements per pass share each read)
-    for (int i0 = threadIdx.x; i0 < (small ? 0 : m); i0 += 4 * blockDim.x) {
-      int idx[4];
-      double vi[4];
-      int rk[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        idx[u] = i0 + u * (int)blockDim.x;
-        vi[u] = idx[u] < m ? sob[idx[u]] : 0.0;
-        rk[u] = 0;
-      }
-      for (int j = 0; j < m; ++j) {
-        const double vj = sob[j];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) rk[u] += before(vj, j, vi[u], idx[u]) ? 1 : 0;
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (idx[u] < m) {
-          const int r = rk[u] + (rk[u] >= pos ? 1 : 0);
-          mu[r] = vi[u];
-          w[r] = lfw ? lf_weight(idx[u], m, lf) : 1.0;
-        }
-      }
-    }
-    if (threadIdx.x == 0) { mu[pos] = pm; w[pos] = prior_weight; }
-    __syncthreads();
-    STAMP(slot, 4);
-    const int K = m + 1;
-    for (int k = threadIdx.x; k < K; k += blockDim.x) {
-      double s;
-      if (k == 0) s = mu[1] - mu[0];
-      else if (k == K - 1) s = mu[K - 1] - mu[K - 2];
-      else s = np_maximum(mu[k] - mu[k - 1], mu[k + 1] - mu[k]);
-      sg[k] = s;
-    }
-  }
-  __syncthreads();
-  const int K = m + 1;
-  // clip (tpe.py:456-462): prior_sigma / min(100, 1 + K)
-  const double hi = ps / 1.0;
-  const double lo = ps / fmin(100.0, 1.0 + (double)K);
-  for (int k = threadIdx.x; k < K; k += blockDim.x)
-    sg[k] = np_minimum(np_maximum(sg[k], lo), hi);
-  __syncthreads();
-  if (threadIdx.x == 0) sg[pos] = ps;
-  __syncthreads();
-  STAMP(slot, 5);
-  const double tot = block_np_sum(w, K, sm.np);
-  for (int k = threadIdx.x; k < K; k += blockDim.x) w[k] = w[k] / tot;
-  if (threadIdx.x == 0) { info[slot].K = K; info[slot].kind = 0; }
-  __syncthreads();
-  STAMP(slot, 6);
-  prep_slot(H, slot, w, mu, sg, info, coef, kcap, scratch2, sm.np);
-  __syncthreads();
-  STAMP(slot, 10);
-}
-
-// ------------------------------------------------------------------------
-// per-component lpdf constants + p_accept, one block per (hp, side)
-// ------------------------------------------------------------------------
-__device__ __forceinline__ double normal_cdf(double x, double mu, double sigma) {
-#pragma clang fp contract(off)
-  const double bottom = np_maximum(1.4142135623730951 * sigma, kEPS);
-  const double z = (x - mu) / bottom;
-  return 0.5 * (1.0 + erf(z));
-}
-
-// Per-component lpdf constants + truncation mass of one slot (block-wide).
-__device__ void prep_slot(const tpe_hp &H, int64_t slot, const double *w, const double *mu,
-                          const double *sg, MixInfo *info, Coef *coef, int64_t kcap,
-                          double *scratch, NpSumSmem &np) {
-#pragma clang fp contract(off)
-  const int K = info[slot].K;
-  Coef *cf = coef + slot * kcap;
-  double *tmp = scratch + slot * kcap;
-  const double wsum = block_np_sum(w, K, np);
-  STAMP(slot, 7);
-  if (H.family == TPE_CAT) {
-    for (int k = threadIdx.x; k < K; k += blockDim.x) {
-      Coef c; c.x = log(w[k]); c.y = 0.0; c.z = 0.0; c.w = 0.0;
-      cf[k] = c;
-    }
-    if (threadIdx.x == 0) {
-      info[slot].kind = 2; info[slot].p_accept = 1.0; info[slot].log_pacc = 0.0;
-      info[slot].wsum = wsum;
-    }
-    __syncthreads();
-    STAMP(slot, 9);
-    return;
-  }
-  const bool bounded = (H.flags & (TPE_HAS_LOW | TPE_HAS_HIGH)) != 0;
-  double pacc = 1.0;
-  if (bounded) {  // tpe.py:130-136 / 273-276 (log-space bounds for LGMM)
-    for (int k = threadIdx.x; k < K; k += blockDim.x)
-      tmp[k] = w[k] * (normal_cdf(H.high, mu[k], sg[k]) - normal_cdf(H.low, mu[k], sg[k]));
-    __syncthreads();
-    pacc = block_np_sum(tmp, K, np);
-  }
-  STAMP(slot, 8);
-  const bool quant = (H.flags & TPE_HAS_Q) != 0;
-  const double L2E = 1.4426950408889634;  // log2(e)
-  const double A0 = sqrt(0.5 * L2E);
-  for (int k = threadIdx.x; k < K; k += blockDim.x) {
-    Coef c;
-    const double s = sg[k];
-    const double sp = np_maximum(s, kEPS);
-    c.x = mu[k];
-    c.w = 0.0;
-    if (quant) {
-      c.y = 1.0 / np_maximum(1.4142135623730951 * s, kEPS);
-      c.z = w[k];
-    } else if (H.family == TPE_GMM) {
-      // log(w / sqrt(2 pi sigma^2) / p_accept), tpe.py:140-144
-      const double Z = sqrt(2.0 * 3.141592653589793 * (s * s));
-      c.y = A0 / sp;
-      c.z = L2E * log(w[k] / Z / pacc);
-    } else {
-      // lognormal_lpdf + log w, minus log(x) per candidate, tpe.py:193-202, 280
-      c.y = A0 / sp;
-      c.z = L2E * (log(w[k]) - log(sp * 2.5066282746310002));
-    }
-    cf[k] = c;
-  }
-  if (threadIdx.x == 0) {
-    info[slot].kind = quant ? 1 : 0;
-    info[slot].p_accept = pacc;
-    info[slot].log_pacc = log(pacc);
-    info[slot].wsum = wsum;
-  }
-}
-
-// Constants of explicitly given mixtures (operator-level tpe_score/lpdf).
-__global__ __launch_bounds__(256) void k_prep(
-    const tpe_hp *__restrict__ hps, const double *__restrict__ mw,
-    const double *__restrict__ mmu, const double *__restrict__ msig,
-    MixInfo *__restrict__ info, Coef *__restrict__ coef, int64_t kcap,
-    double *__restrict__ scratch) {
-  __shared__ NpSumSmem np;
-  const int hp = blockIdx.x, side = blockIdx.y;
-  const int64_t slot = 2 * (int64_t)hp + side;
-  const tpe_hp H = hps[hp];
-  prep_slot(H, slot, mw + slot * kcap, mmu + slot * kcap, msig + slot * kcap, info, coef, kcap,
-            scratch, np);
-}
+constexpr int kSortMax = 8192;  // candidates per bucketing chunk
 
 // ------------------------------------------------------------------------
 // counter-based Philox4x32-10 in registers
@@ -1158,13 +541,6 @@ __global__ __launch_bounds__(256) void k_micro(int iters, double *sink) {
   }
 }
 
-#ifdef TPE_STAMPS
-}  // namespace tpe
-extern "C" int tpe_debug_stamps(unsigned long long *out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(tpe::g_stamps), sizeof(tpe::g_stamps)) == hipSuccess ? 0 : -5;
-}
-namespace tpe {
-#endif
 
 hipError_t launch_micro(int which, int blocks, int iters, double *sink, hipStream_t st) {
   switch (which) {
@@ -1178,34 +554,6 @@ hipError_t launch_micro(int which, int blocks, int iters, double *sink, hipStrea
 // ------------------------------------------------------------------------
 // launch wrappers
 // ------------------------------------------------------------------------
-hipError_t launch_split(const double *losses, int64_t n, int32_t n_below, uint8_t *below,
-                        hipStream_t st) {
-  const size_t lds = n <= kSortMax ? (size_t)kSortMax * 12 : 0;
-  k_split<<<1, 1024, lds, st>>>(losses, n, n_below, below);
-  return hipGetLastError();
-}
-
-hipError_t launch_fit(const tpe_hp *hps, int32_t n_hp, const double *vals,
-                      const uint8_t *active, const double *losses, int64_t n, int32_t n_below,
-                      double prior_weight, int32_t lf, const double *pprior, double *mw,
-                      double *mmu, double *msig, MixInfo *info, Coef *coef, int64_t kcap,
-                      double *scratch, double *scratch2, hipStream_t st) {
-  if (n_hp <= 0) return hipSuccess;
-  const size_t lds = (size_t)12288 * 8;  // 96 KB: see the k_fit LDS layout
-  k_fit<<<dim3(n_hp, 2), 1024, lds, st>>>(hps, vals, active, losses, n, n_below, prior_weight, lf,
-                                          pprior, mw, mmu, msig, info, coef, kcap, scratch,
-                                          scratch2);
-  return hipGetLastError();
-}
-
-hipError_t launch_prep(const tpe_hp *hps, int32_t n_hp, const double *mw, const double *mmu,
-                       const double *msig, MixInfo *info, Coef *coef, int64_t kcap,
-                       double *scratch, hipStream_t st) {
-  if (n_hp <= 0) return hipSuccess;
-  k_prep<<<dim3(n_hp, 2), 256, 0, st>>>(hps, mw, mmu, msig, info, coef, kcap, scratch);
-  return hipGetLastError();
-}
-
 hipError_t launch_score(const ScoreArgs &a, int32_t kind, int32_t grid_x, hipStream_t st) {
   if (a.n_slots <= 0) return hipSuccess;
   if (a.n_suggest <= 0) return hipSuccess;

@@ -118,6 +118,10 @@ class ShardedSuggest(object):
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.device = torch.device('cuda', plan.engine.device)
+        # a real (non-null) stream shared by the engine launches, the record
+        # copies and the collective: stream 0 would mean "the engine's own
+        # stream" at the C ABI and leave torch unordered with it
+        self.stream = torch.cuda.Stream(self.device)
         self.gather = lambda t: gather_records(t, self.group)
 
     def suggest(self, seeds, n_cand, fetch=True):
@@ -125,14 +129,17 @@ class ShardedSuggest(object):
         seeds = np.ascontiguousarray(np.atleast_1d(seeds), dtype=np.uint64)
         S, P = seeds.size, self.plan.n_hp
         begin, count = shard_range(int(n_cand), self.rank, self.world)
-        stream = torch.cuda.current_stream(self.device).cuda_stream
-        local = torch.empty(S * P * RECORD_BYTES, dtype=torch.uint8, device=self.device)
-        for level in range(self.plan.n_levels):
-            self.plan.suggest(seeds, count, cand_begin=begin, level=level, out=local.data_ptr(),
-                              stream=stream)
-            gathered = self.gather(local)
-            self.plan.merge(gathered.data_ptr(), self.world, level, out=local.data_ptr(),
-                            stream=stream, n_suggest=S)
-        if not fetch:
-            return local
-        return local.cpu().numpy().view(E.RESULT_DTYPE).reshape(S, P)
+        stream = self.stream.cuda_stream
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.stream):
+            local = torch.empty(S * P * RECORD_BYTES, dtype=torch.uint8, device=self.device)
+            for level in range(self.plan.n_levels):
+                self.plan.suggest(seeds, count, cand_begin=begin, level=level,
+                                  out=local.data_ptr(), stream=stream)
+                gathered = self.gather(local)
+                self.plan.merge(gathered.data_ptr(), self.world, level, out=local.data_ptr(),
+                                stream=stream, n_suggest=S)
+            if not fetch:
+                torch.cuda.current_stream(self.device).wait_stream(self.stream)
+                return local
+            return local.cpu().numpy().view(E.RESULT_DTYPE).reshape(S, P)

@@ -189,3 +189,43 @@ def test_categorical_sampler(eng):
     x = eng.sample(CAT, p, seed=5, n=200000)
     freq = np.bincount(x.astype(int), minlength=4) / x.size
     assert np.allclose(freq, p, atol=5e-3)
+
+
+# ---- fit tiers of tpe_fit.hip: tiny (<= 64, one wave), LDS radix sort
+# (<= 10240), global radix sort (> 10240); mixtures in LDS (K <= 4097) or HBM
+@pytest.mark.parametrize('n', [2, 63, 64, 65, 1000, 4096, 4097, 10240, 10241, 30000])
+@pytest.mark.parametrize('ties', [False, True])
+def test_parzen_sort_tiers_bit_exact(eng, n, ties):
+    rng = np.random.RandomState(n + ties)
+    obs = rng.uniform(-5, 5, n)
+    if ties:
+        obs = np.round(obs)                          # heavy ties: stable order matters
+        obs[::7] = -0.0                              # -0.0 ties +0.0 (numpy order)
+    w, mu, sg = eng.parzen_fit(obs, 1.0, 0.25, 10.0)
+    ref = O.parzen_fit(obs, 1.0, 0.25, 10.0, kind='stable')
+    np.testing.assert_array_equal(mu, ref[1])
+    np.testing.assert_array_equal(sg, ref[2])
+    np.testing.assert_array_equal(w, ref[0])
+
+
+@pytest.mark.parametrize('n,gamma,cap', [(1000, 0.25, 25), (20000, 0.25, 25), (5000, 2.0, 1000),
+                                         (30000, 1.0, 1000), (50, 10.0, 1000)])
+def test_split_rounds_and_sort_paths(eng, n, gamma, cap):
+    rng = np.random.RandomState(n)
+    losses = np.round(rng.rand(n), 3)                # ties
+    losses[rng.randint(n, size=5)] = np.inf          # pending trials
+    losses[rng.randint(n, size=2)] = np.nan
+    mask = eng.split(losses, gamma, gamma_cap=cap)
+    good, _ = O.below_tids(np.arange(n), losses, gamma, gamma_cap=cap, kind='stable')
+    assert set(np.where(mask)[0].tolist()) == good
+
+
+@pytest.mark.parametrize('n,upper', [(0, 3), (10, 3), (20000, 7), (5000, 300), (3000, 5000)])
+def test_categorical_posterior_sizes(eng, n, upper):
+    rng = np.random.RandomState(upper)
+    obs = rng.randint(0, min(upper, 40), n)
+    p = eng.categorical_posterior(obs, upper, 1.0)
+    np.testing.assert_array_equal(p, O.categorical_posterior(obs, upper, 1.0))
+    pp = rng.dirichlet(np.ones(upper))
+    p = eng.categorical_posterior(obs, upper, 0.5, pp)
+    np.testing.assert_array_equal(p, O.categorical_posterior(obs, upper, 0.5, pp))

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Per-phase timing of k_fit from the TPE_STAMPS debug build
-(make -C hyperopt_amd/csrc dbg).  Prints, per (hp, side) slot, the µs spent
-in each phase of the last fit.  Diagnostic only."""
+"""Per-phase timing of k_fit from the TPE_STAMPS diagnostic build
+(make -C hyperopt_amd/csrc dbg): for each (hp, side) slot of the last fit,
+the time (us from the slot's start) at which each phase ended.  Diagnostic
+only; the product library has no stamps."""
 import ctypes as C
 import os
 import sys
@@ -14,15 +15,15 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 from hyperopt_amd import _engine as E  # noqa: E402
 
-PH = ['split', 'gather', 'lds', 'sort/bincount', 'sigma', 'normalise', 'wsum', 'pacc', 'end_cat',
-      'end']
+PH = {11: 'keys', 12: 'd1', 13: 'd2', 14: 'd3', 15: 'd4', 1: 'split', 2: 'gather', 3: 'sort', 4: 'place', 5: 'sigma/bins', 6: 'norm', 7: 'wsum',
+      8: 'pacc', 10: 'end'}
 
 
-def main(cfg):
+def main(cfg, slots):
     import torch
     torch.cuda.set_device(0)
     eng = E.Engine(0)
-    dom, losses, vals, active, n_cand = bench.build_workload(cfg)
+    dom, losses, vals, active, _ = bench.build_workload(cfg)
     hps, conds, pprior = dom.space.engine_tables()
     plan = E.Plan(eng, hps, conds, pprior, max_trials=losses.size)
     plan.set_history(losses, vals, active)
@@ -35,17 +36,16 @@ def main(cfg):
     P = len(dom.space.labels)
     t0 = st[:2 * P, 0].min()
     print(cfg, 'P=%d N=%d' % (P, losses.size))
-    for slot in range(2 * P):
+    for slot in range(min(2 * P, slots)):
         row = st[slot]
         h = dom.space.hps[slot // 2]
-        marks = [(PH[i - 1], (row[i] - row[0]) / 100.0) for i in range(1, 11) if row[i] >= row[0]]
-        print('%-8s %-10s side=%d start=%6.1fus ' % (h.label[:8], h.dist[:10], slot % 2,
-                                                     (row[0] - t0) / 100.0) +
-              ' '.join('%s=%.1f' % m for m in marks))
-    end = max(st[s, 10] if st[s, 10] else st[s, 9] for s in range(2 * P))
-    print('kernel span (first start -> last end): %.1f us' % ((end - t0) / 100.0))
+        marks = ['%s=%.1f' % (PH[i], (row[i] - row[0]) / 100.0) for i in [11, 12, 13, 14, 15] + sorted(k for k in PH if k < 11)
+                 if row[i] >= row[0]]
+        print('%-8s %-10s side=%d start=%5.1f ' % (h.label[:8], h.dist[:10], slot % 2,
+                                                   (row[0] - t0) / 100.0) + ' '.join(marks))
+    print('kernel span: %.1f us' % ((st[:2 * P, 10].max() - t0) / 100.0))
 
 
 if __name__ == '__main__':
     for c in sys.argv[1:] or ['cfg2']:
-        main(c)
+        main(c, 40)
