@@ -105,6 +105,8 @@ def main():
     ap.add_argument('--warmup', type=int, default=10)
     ap.add_argument('--config', default='cfg2', choices=['cfg2', 'cfg3', 'cfg4'])
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
+    ap.add_argument('--n-cand', type=int, default=0,
+                    help='override candidates per suggest (secondary measurements only)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--traffic-json', default=os.path.join(ROOT, 'profiles', 'traffic.json'))
     args = ap.parse_args()
@@ -122,6 +124,8 @@ def main():
     from hyperopt_amd import _engine as E
     eng = E.Engine(local)
     dom, losses, vals, active, n_cand = build_workload(args.config)
+    if args.n_cand:
+        n_cand = args.n_cand
     hps, conds, pprior = dom.space.engine_tables()
     plan = E.Plan(eng, hps, conds, pprior, max_trials=losses.size)
     # history resident in HBM before the timed region
@@ -140,7 +144,6 @@ def main():
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
-    plan.profile(args.steps)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -155,48 +158,70 @@ def main():
     if dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
-
     _, pairs_step = plan.last_stats()
-    kernels = {}
+    value = world * pairs_step * args.steps / elapsed
+
+    # ---- profiled pass (after the timed region): HIP events on the engine
+    # stream around every scoring launch, and the quantized-pair census
+    n_prof = max(1, min(args.steps, 20))
+    plan.profile(n_prof)
+    for i in range(n_prof):
+        step(args.warmup + args.steps + i)
+    kinds = {}
+    score_ms, launches = 0.0, 0
     for kind, name in enumerate(E.KIND_NAMES):
         ms, n, pairs = plan.profile_read(kind)
-        if n:
-            kernels[name] = dict(avg_ms=ms, launches_per_step=n / args.steps,
-                                 pairs_per_launch=pairs,
-                                 pairs_per_s=(pairs / (ms * 1e-3)) if ms > 0 else None)
-    value = world * pairs_step * args.steps / elapsed
+        score_ms, launches = ms, n
+        if pairs:
+            kinds[name] = pairs
+    plan.profile(0)
+    # census pass (its counting variant of the kernel is not timed)
+    plan.census(True)
+    for i in range(n_prof):
+        step(args.warmup + args.steps + n_prof + i)
+    census = plan.census(False)
 
     if rank != 0:
         if dist:
             dist.destroy_process_group()
         return
-    # ---- roofline of the dominant scoring kernel ------------------------------
-    dom_name = max(kernels, key=lambda k: kernels[k]['avg_ms'] * kernels[k]['launches_per_step'])
-    kd = kernels[dom_name]
-    pps = kd['pairs_per_s'] or 0.0
-    if dom_name.startswith('erf'):
-        peak = eng.microbench(2)            # OCML fp64 erf / s, register-only
-        roof = dict(bound='transcendental', unit='Gerf/s', achieved=2 * pps / 1e9,
-                    peak=peak / 1e9, note='2 fp64 erf per pair (tpe.py:146-160); peak = '
-                    'measured register-only OCML erf rate')
-    else:
-        peak = eng.microbench(1)            # fp64 FMA flop/s
-        roof = dict(bound='valu', unit='TFLOP/s', achieved=6 * pps / 1e12, peak=peak / 1e12,
-                    note='6 fp64 flops + 1 exp per pair (SURVEY 8d); peak = measured '
-                    'register-only fp64 FMA rate')
-    roof['frac'] = roof['achieved'] / roof['peak'] if roof['peak'] else None
-    roof['kernel'] = 'k_score<%s>' % dom_name
-    roof['avg_launch_ms'] = kd['avg_ms']
-    roof['pairs_per_launch'] = kd['pairs_per_launch']
+    # ---- roofline of the dominant kernel, k_score (every lpdf kind of the
+    # level in one launch).  Work is priced at the measured register-only
+    # rate of exactly its pair arithmetic: log-sum-exp pairs (2 FMA + max +
+    # exp2 + fp64 sum) and evaluated quantized pairs (2 fp64 erf); quantized
+    # pairs that are exact zeros for the whole wave are skipped by the
+    # algorithm and cost no erf.
+    lse_peak = eng.microbench(3)
+    erf_peak = eng.microbench(4)
+    lse_pairs = kinds.get('lse_gmm', 0.0) + kinds.get('lse_lgmm', 0.0)
+    erf_pairs = kinds.get('erf_gmm', 0.0) + kinds.get('erf_lgmm', 0.0)
+    per_launch = max(1, launches)
+    erf_exec = census[2] / per_launch
+    t_kernel = score_ms * 1e-3
+    t_peak = lse_pairs / lse_peak + erf_exec / erf_peak
+    achieved = (lse_pairs + erf_exec * lse_peak / erf_peak) / t_kernel if t_kernel else 0.0
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
             with open(args.traffic_json) as f:
-                traffic = json.load(f).get(args.config, {}).get(dom_name)
+                traffic = json.load(f).get(args.config, {}).get('score')
         except Exception:
             traffic = None
-    roof['traffic'] = traffic
-    roof['exp_peak_per_s'] = eng.microbench(0)
+    roof = dict(bound='valu', unit='Gpair/s', achieved=achieved / 1e9, peak=lse_peak / 1e9,
+                frac=(t_peak / t_kernel) if t_kernel else None, traffic=traffic,
+                kernel='k_score (all lpdf kinds of a level, one launch)',
+                avg_launch_ms=score_ms, launches_per_step=launches / n_prof,
+                note='unit = log-sum-exp-pair equivalents: achieved = (LSE pairs + evaluated '
+                     'quantized pairs x lse_peak/erf_peak) / launch time; peaks are '
+                     'register-only microkernels of exactly the pair arithmetic (LSE pair: 2 '
+                     'fp64 FMA + max + v_exp_f32 + fp64 sum, SURVEY 8d "1 exp + 6 flops"; '
+                     'quantized pair: 2 OCML fp64 erf + 8 flops)',
+                lse_pairs_per_launch=lse_pairs, erf_pairs_per_launch=erf_pairs,
+                erf_live_pairs_per_launch=census[1] / per_launch,
+                erf_evaluated_pairs_per_launch=erf_exec,
+                lse_pair_peak_per_s=lse_peak, erf_pair_peak_per_s=erf_peak,
+                fp64_fma_peak_flops=eng.microbench(1), exp_f32_peak_per_s=eng.microbench(0),
+                erf_f64_peak_per_s=eng.microbench(2))
 
     cpu = None
     if not args.no_cpu_baseline and world == 1:
@@ -221,12 +246,12 @@ def main():
                                  'candidates/suggest', 'cfg3': 'config 3: 50-hp conditional, '
                                  '1e4 history, 1e5 candidates', 'cfg4': 'config 4: 100-D, 1e4 '
                                  'history, 1e7 candidates'}[args.config],
+            'candidates_per_suggest': n_cand,
             'pairs_per_suggest': pairs_step,
             'suggest_latency_ms': 1e3 * elapsed / args.steps,
             'parallelism': 'replicas' if world > 1 else 'single',
         },
         'roofline': roof,
-        'kernels': kernels,
         'cpu_baseline': cpu,
     }
     print(json.dumps(line))

@@ -38,7 +38,7 @@ EXPORTS = (
     'tpe_plan_num_levels', 'tpe_plan_set_history', 'tpe_plan_fit', 'tpe_plan_get_mixture',
     'tpe_plan_suggest', 'tpe_plan_merge', 'tpe_plan_score_candidates', 'tpe_plan_last_stats',
     'tpe_plan_profile', 'tpe_plan_profile_read', 'tpe_microbench', 'tpe_plan_get_results',
-    'tpe_plan_results_device',
+    'tpe_plan_results_device', 'tpe_plan_census',
 )
 
 
@@ -138,6 +138,7 @@ def load_library(path: str = LIB_PATH):
             'tpe_microbench': (C.c_int, [vp, i32, _D]),
             'tpe_plan_get_results': (C.c_int, [vp, vp, i32, vp]),
             'tpe_plan_results_device': (vp, [vp]),
+            'tpe_plan_census': (C.c_int, [vp, i32, C.POINTER(i64)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -431,6 +432,15 @@ class Plan(object):
             e.check(e.lib.tpe_plan_profile_read(self.p, int(kind), C.byref(ms), C.byref(n),
                                                 C.byref(pairs)))
         return ms.value, n.value, pairs.value
+
+    def census(self, enable):
+        """Quantized-pair census since the last call (total, live, evaluated);
+        enable it for the following suggests."""
+        e = self.engine
+        out = (C.c_int64 * 3)()
+        with e.lock:
+            e.check(e.lib.tpe_plan_census(self.p, int(bool(enable)), out))
+        return tuple(int(v) for v in out)
 
     def last_stats(self):
         e = self.engine

@@ -41,4 +41,76 @@ __device__ __forceinline__ bool kp_less(uint64_t ka, uint32_t pa, uint64_t kb, u
   return ka < kb || (ka == kb && pa < pb);
 }
 
+// numpy argmax order over (score, global index): a NaN wins at its first
+// index, otherwise the larger score, ties to the lower index (tpe.py:756).
+__device__ __forceinline__ bool better(double sa, int64_t ia, double sb, int64_t ib) {
+  if (ia < 0) return false;
+  if (ib < 0) return true;
+  const bool na = sa != sa, nb = sb != sb;
+  if (na || nb) return (na && nb) ? ia < ib : na;
+  if (sa != sb) return sa > sb;
+  return ia < ib;
+}
+
+__device__ __forceinline__ void wave_best(double &s, double &v, int64_t &i) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double os = __shfl_xor(s, o, 64);
+    const double ov = __shfl_xor(v, o, 64);
+    const int64_t oi = __shfl_xor(i, o, 64);
+    if (better(os, oi, s, i)) { s = os; v = ov; i = oi; }
+  }
+}
+
+// activity of a conditional hp: OR over its (parent active and parent value
+// == branch) conditions (hyperopt/vectorize.py:20-38 routing)
+__device__ __forceinline__ bool hp_active(const tpe_hp &H, const Partial *res,
+                                          const int32_t *cp, const int32_t *cb) {
+  if (H.cond_count == 0) return true;
+  for (int c = 0; c < H.cond_count; ++c) {
+    const Partial &r = res[cp[H.cond_begin + c]];
+    if (r.active && r.index >= 0 && r.value == (double)cb[H.cond_begin + c]) return true;
+  }
+  return false;
+}
+
+// Per-component scoring coefficients (Coef, 32 B) of a continuous mixture.
+//  LSE (q = None): the log-density term in log2 units as a quadratic in the
+//   centred candidate y' = y - center (center = prior_mu of the hp):
+//     t = c - (a (y' - mu'))^2 = alpha + y' (beta + gamma y'),
+//   a = sqrt(log2(e) / 2) / max(sigma, EPS), mu' = mu - center,
+//   c = log2(e) log(w / sqrt(2 pi sigma^2) / p_accept)      (GMM1_lpdf, tpe.py:138-144)
+//   c = log2(e) (log w - log(max(sigma, EPS) sqrt(2 pi)))   (LGMM1_lpdf, tpe.py:193-202,
+//       278-281: no p_accept; log x is subtracted per candidate).
+//   Centring keeps alpha, beta y' and gamma y'^2 within ~(100 |mu'| / range)^2 of
+//   t, i.e. cancellation costs < 1e-12 absolute in fp64.
+//  ERF (q given): (mu, 1 / max(sqrt(2) sigma, EPS), w) for the CDF differences.
+__device__ __forceinline__ Coef make_coef(const tpe_hp &H, double w, double mu, double sigma,
+                                          double pacc) {
+#pragma clang fp contract(off)
+  Coef c;
+  c.w = 0.0;
+  const double sp = np_maximum(sigma, kEPS);
+  if (H.flags & TPE_HAS_Q) {
+    c.x = mu;
+    c.y = 1.0 / np_maximum(1.4142135623730951 * sigma, kEPS);
+    c.z = w;
+    return c;
+  }
+  const double L2E = 1.4426950408889634;  // log2(e)
+  double cc;
+  if (H.family == TPE_GMM) {
+    const double Z = sqrt(2.0 * 3.141592653589793 * (sigma * sigma));
+    cc = L2E * log(w / Z / pacc);
+  } else {
+    cc = L2E * (log(w) - log(sp * 2.5066282746310002));
+  }
+  const double a2 = (0.5 * L2E) / (sp * sp);   // a^2
+  const double m = mu - H.prior_mu;            // mu'
+  c.x = cc - a2 * (m * m);                     // alpha
+  c.y = 2.0 * a2 * m;                          // beta
+  c.z = -a2;                                   // gamma
+  return c;
+}
+
 }  // namespace tpe

@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -55,6 +56,8 @@ struct tpe_plan {
   uint64_t *d_seeds = nullptr;
   Partial *d_partial = nullptr;
   size_t partial_cap = 0;
+  unsigned long long *d_census = nullptr;  // [3] quantized-pair census (tpe_plan_census)
+  bool census = false;
   uint32_t *d_ticket = nullptr;
   std::vector<uint64_t> h_seeds;  // this call's seeds (inline kernel args when <= 8)
   bool has_erf = false;
@@ -113,7 +116,7 @@ void plan_free_buffers(tpe_plan *p) {
                   p->d_losses, p->d_vals, p->d_active, p->d_below, p->d_mw, p->d_mmu,
                   p->d_msig, p->d_scratch, p->d_info, p->d_coef, p->d_results, p->d_seeds,
                   p->d_partial, p->d_ext, p->d_lb, p->d_la, p->d_cand, p->d_cpos,
-                  p->d_ticket, p->d_sortbuf};
+                  p->d_ticket, p->d_sortbuf, p->d_census};
   for (void *b : bufs) dfree(b);
   if (p->ev0) (void)hipEventDestroy(p->ev0);
   if (p->ev1) (void)hipEventDestroy(p->ev1);
@@ -207,6 +210,7 @@ int plan_build(tpe_engine *h, const tpe_space *sp, int64_t max_trials, tpe_plan 
   if (max_trials < 0) return fail(h, TPE_E_INVALID, "max_trials < 0");
   p->eng = h;
   p->P = sp->n_hp;
+
   p->hps.assign(sp->hp, sp->hp + sp->n_hp);
   p->cond_parent.assign(sp->cond_parent, sp->cond_parent + sp->n_cond);
   p->cond_branch.assign(sp->cond_branch, sp->cond_branch + sp->n_cond);
@@ -241,6 +245,8 @@ int plan_build(tpe_engine *h, const tpe_space *sp, int64_t max_trials, tpe_plan 
   p->scap = p->ncap + 1;
   CKH(dalloc(&p->d_sortbuf, (size_t)slots * 16 * p->scap));
   CKH(dalloc(&p->d_info, slots));
+  CKH(dalloc(&p->d_census, 3));
+  CKH(hipMemset(p->d_census, 0, 3 * sizeof(unsigned long long)));
   CKH(dalloc(&p->d_coef, (size_t)slots * kcap));
   CKH(hipEventCreate(&p->ev0));
   CKH(hipEventCreate(&p->ev1));
@@ -300,26 +306,12 @@ int ensure_ext(tpe_engine *h, tpe_plan *p, size_t n) {
   return TPE_OK;
 }
 
-// Component split (ks waves of a 16-wave block share 64 candidates) and grid
-// size for one scoring launch: aim for >= 8 waves per SIMD of the 1024 SIMDs
-// when the candidate count allows, else split the mixtures further.
-void choose_geometry(int64_t n_cand, int64_t n_slots, int64_t n_sug, int32_t kind, int32_t &ks,
-                     int32_t &tiles, int32_t &grid_x) {
-  const int64_t want_waves = 8192;
-  ks = 16;
-  if (kind != KIND_CAT) {
-    for (int c : {1, 2, 4, 8, 16}) {
-      const int64_t groups = (n_cand + 63) / 64;  // 64-candidate groups per (s, hp)
-      if (groups * n_slots * n_sug * c >= want_waves || c == 16) { ks = c; break; }
-    }
-  } else {
-    ks = 1;
-  }
-  const int64_t tc = 64 * (16 / ks);
-  tiles = (int32_t)std::max<int64_t>(0, (n_cand + tc - 1) / tc);
-  const int64_t target_blocks = 256 * 4;  // 1024-thread blocks, a few per CU in flight
-  int64_t per = std::max<int64_t>(1, target_blocks / std::max<int64_t>(1, n_slots * n_sug));
-  grid_x = (int32_t)std::max<int64_t>(1, std::min<int64_t>(std::max(tiles, 1), per));
+// Scoring launch geometry: one 16-wave block per 64-candidate tile.
+struct Geom {
+  int32_t tiles;
+};
+Geom score_geometry(int64_t n_cand) {
+  return Geom{(int32_t)std::max<int64_t>(0, (n_cand + kTile - 1) / kTile)};
 }
 
 int ensure_cand(tpe_engine *h, tpe_plan *p, size_t n) {
@@ -356,6 +348,7 @@ ScoreArgs base_args(tpe_plan *p, int64_t n_sug) {
   a.results = p->d_results;
   a.partial = p->d_partial;
   a.ticket = p->d_ticket;
+  a.census = p->census ? p->d_census : nullptr;
   a.kcap = p->kcap;
   a.n_hp = p->P;
   a.n_suggest = (int32_t)n_sug;
@@ -386,32 +379,35 @@ FitArgs fit_args(tpe_plan *p, int32_t n_below, double prior_weight, int32_t lf) 
   return a;
 }
 
-int score_launch(tpe_engine *h, tpe_plan *p, ScoreArgs a, int32_t kind, int32_t grid_x,
-                 int64_t cn, hipStream_t sg, bool record) {
+int score_launch(tpe_engine *h, tpe_plan *p, ScoreArgs a, bool has_erf, int64_t cn,
+                 hipStream_t sg, bool record) {
   tpe_plan::Prof *pr = nullptr;
   if (record && p->prof_cap > 0) {
-    pr = &p->prof[kind];
+    pr = &p->prof[0];
     if (pr->n >= p->prof_cap) pr = nullptr;  // ring full: stop recording
   }
   if (pr) CKH(hipEventRecord(pr->a[pr->n], sg));
-  CKH(launch_score(a, kind, grid_x, sg));
+  CKH(launch_score(a, has_erf, sg));
   if (pr) {
     CKH(hipEventRecord(pr->b[pr->n], sg));
-    pr->pairs[pr->n] = group_pairs(p, kind, a.n_slots, cn, a.n_suggest);
+    pr->pairs[pr->n] = (double)cn * (double)a.n_suggest;
     pr->n++;
   }
   return TPE_OK;
 }
 
-// One level of conditional hps: one draw(+sort) launch for all of its hps,
-// then one fused score+argmax launch per lpdf kind, the kinds running
-// concurrently on the engine's auxiliary streams.  Candidates are processed
-// in chunks so the buffer stays <= 512 MB.
+// One level of conditional hps: one draw(+bucket) launch and one scoring
+// launch (every lpdf kind) for all of its hps.  Candidates are processed in
+// chunks so the buffer stays <= 512 MB.
 int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_cand,
               int64_t cand_begin, hipStream_t st) {
-  const auto &groups = p->groups[level];
   const int32_t n_level = (int32_t)p->levels[level].size();
   const int32_t *lvl = p->d_level_hps + p->level_off[level];
+  bool erf_level = false;
+  for (int hp : p->levels[level]) {
+    const int k = score_kind(p->hps[hp]);
+    erf_level |= k == KIND_ERF_G || k == KIND_ERF_L;
+  }
   const int64_t budget = (int64_t)64 << 20;  // doubles
   const int64_t chunk = std::max<int64_t>(
       1, std::min<int64_t>(std::max<int64_t>(n_cand, 1),
@@ -419,13 +415,8 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
   int64_t c0 = 0;
   do {
     const int64_t cn = std::min(chunk, n_cand - c0);
-    std::vector<int32_t> ks(groups.size()), tiles(groups.size()), gx(groups.size());
-    int32_t pstride = 1;
-    for (size_t g = 0; g < groups.size(); ++g) {
-      choose_geometry(cn, groups[g].count, n_sug, groups[g].kind, ks[g], tiles[g], gx[g]);
-      pstride = std::max(pstride, gx[g]);
-    }
-    int rc = ensure_suggest_state(h, p, n_sug, (size_t)n_sug * p->P * pstride);
+    const Geom geo = score_geometry(cn);
+    int rc = ensure_suggest_state(h, p, n_sug, (size_t)n_sug * p->P * std::max(1, geo.tiles));
     if (rc) return rc;
     rc = ensure_cand(h, p, (size_t)std::max<int64_t>(1, n_sug * n_level * cn));
     if (rc) return rc;
@@ -434,34 +425,19 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
     a.cand_sstride = (int64_t)n_level * cn;
     a.n_cand = cn;
     a.cand_begin = cand_begin + c0;
-    a.pstride = pstride;
+    a.pstride = std::max(1, geo.tiles);
     a.accumulate = c0 > 0 ? 1 : 0;
     a.level_hps = lvl;
     a.n_slots = n_level;
+    a.cand_slot0 = 0;
+    a.tiles = geo.tiles;
     for (int i = 0; i < kInlineSeeds && i < n_sug; ++i) a.seed_inline[i] = p->h_seeds[i];
     a.n_inline_seeds = (int32_t)std::min<int64_t>(n_sug, kInlineSeeds);
     CKH(launch_draw(a, st));
-    if (p->has_erf) CKH(launch_bucket(a, p->d_cpos, st));
-    const bool fork = groups.size() > 1;
-    if (fork) CKH(hipEventRecord(p->ev_fork, st));
-    for (size_t g = 0; g < groups.size(); ++g) {
-      hipStream_t sg = (g == 0 || g > (size_t)tpe_engine::kAux) ? st : h->aux[g - 1];
-      if (sg != st) CKH(hipStreamWaitEvent(sg, p->ev_fork, 0));
-      ScoreArgs b = a;
-      const int32_t rel = groups[g].off - p->level_off[level];
-      b.level_hps = lvl + rel;
-      b.n_slots = groups[g].count;
-      b.cand_slot0 = rel;
-      b.cand_pos = (groups[g].kind == KIND_ERF_G || groups[g].kind == KIND_ERF_L) ? p->d_cpos
-                                                                                     : nullptr;
-      b.ks = ks[g];
-      b.tiles = tiles[g];
-      rc = score_launch(h, p, b, groups[g].kind, gx[g], cn, sg, true);
-      if (rc) return rc;
-      if (sg != st) CKH(hipEventRecord(p->ev_join[g % 8], sg));
-    }
-    for (size_t g = 1; g < groups.size() && g <= (size_t)tpe_engine::kAux; ++g)
-      CKH(hipStreamWaitEvent(st, p->ev_join[g % 8], 0));
+    if (erf_level) CKH(launch_bucket(a, p->d_cpos, st));
+    a.cand_pos = erf_level ? p->d_cpos : nullptr;
+    rc = score_launch(h, p, a, erf_level, cn, st, true);
+    if (rc) return rc;
     c0 += cn;
   } while (c0 < n_cand);
   return TPE_OK;
@@ -471,23 +447,21 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
 int run_external(tpe_engine *h, tpe_plan *p, int32_t hp, const double *ext, int64_t n,
                  double *lb, double *la, hipStream_t st) {
   const int kind = score_kind(p->hps[hp]);
-  int32_t ks, tiles, gx;
-  choose_geometry(n, 1, 1, kind, ks, tiles, gx);
-  int rc = ensure_suggest_state(h, p, 1, (size_t)p->P * gx);
+  const Geom geo = score_geometry(n);
+  int rc = ensure_suggest_state(h, p, 1, (size_t)p->P * std::max(1, geo.tiles));
   if (rc) return rc;
   ScoreArgs a = base_args(p, 1);
   a.cand = ext;
   a.cand_sstride = n;
   a.n_cand = n;
-  a.pstride = gx;
+  a.pstride = std::max(1, geo.tiles);
   a.level_hps = p->d_all_hps + hp;
   a.n_slots = 1;
   a.out_lb = lb;
   a.out_la = la;
   a.force_active = 1;
-  a.ks = ks;
-  a.tiles = tiles;
-  return score_launch(h, p, a, kind, gx, n, st, false);
+  a.tiles = geo.tiles;
+  return score_launch(h, p, a, kind == KIND_ERF_G || kind == KIND_ERF_L, n, st, false);
 }
 
 int copy_results(tpe_engine *h, tpe_plan *p, int64_t n_sug, tpe_result *out, int32_t on_dev,
@@ -983,10 +957,11 @@ int tpe_plan_profile_read(tpe_plan_t p, int32_t kind, double *avg_ms, int64_t *l
   tpe_engine *h = p->eng;
   CKH(hipSetDevice(h->device));
   CKH(hipDeviceSynchronize());
-  auto &pr = p->prof[kind];
+  auto &pr = p->prof[0];  // every scoring launch (all lpdf kinds of a level)
   double tot = 0.0, pairs = 0.0;
-  // components per candidate of the kind's hps (all levels), active in the
-  // last suggestion (levels' activity is the same for every profiled step)
+  // this kind's pairs in those launches: components per candidate of the
+  // kind's hps (all levels), active in the last suggestion (levels' activity
+  // is the same for every profiled step)
   std::vector<MixInfo> info(2 * (size_t)p->P);
   std::vector<Partial> res((size_t)std::max<int64_t>(1, p->last_nsug) * p->P);
   CKH(hipMemcpy(info.data(), p->d_info, info.size() * sizeof(MixInfo), hipMemcpyDeviceToHost));
@@ -1009,17 +984,31 @@ int tpe_plan_profile_read(tpe_plan_t p, int32_t kind, double *avg_ms, int64_t *l
   if (avg_ms) *avg_ms = pr.n ? tot / pr.n : 0.0;
   if (launches) *launches = pr.n;
   if (pairs_per_launch) *pairs_per_launch = pr.n ? pairs / pr.n : 0.0;
-  pr.n = 0;
+  return TPE_OK;  // the ring is re-armed by tpe_plan_profile
+}
+
+int tpe_plan_census(tpe_plan_t p, int32_t enable, int64_t *counts) {
+  if (!p) return TPE_E_INVALID;
+  tpe_engine *h = p->eng;
+  CKH(hipSetDevice(h->device));
+  CKH(hipDeviceSynchronize());
+  if (counts) {
+    unsigned long long c[3];
+    CKH(hipMemcpy(c, p->d_census, sizeof(c), hipMemcpyDeviceToHost));
+    for (int i = 0; i < 3; ++i) counts[i] = (int64_t)c[i];
+  }
+  CKH(hipMemset(p->d_census, 0, 3 * sizeof(unsigned long long)));
+  p->census = enable != 0;
   return TPE_OK;
 }
 
 int tpe_microbench(tpe_handle_t h, int32_t which, double *per_second) {
-  if (!h || !per_second || which < 0 || which > 2) return TPE_E_INVALID;
+  if (!h || !per_second || which < 0 || which > 4) return TPE_E_INVALID;
   CKH(hipSetDevice(h->device));
   hipDeviceProp_t prop;
   CKH(hipGetDeviceProperties(&prop, h->device));
   const int blocks = prop.multiProcessorCount * 8;
-  const int iters = which == 2 ? 256 : 4096;
+  const int iters = which == 2 ? 256 : (which == 3 ? 512 : (which == 4 ? 128 : 4096));
   double *sink = nullptr;
   CKH(dalloc(&sink, (size_t)blocks * 256));
   hipEvent_t a, b;
@@ -1035,9 +1024,10 @@ int tpe_microbench(tpe_handle_t h, int32_t which, double *per_second) {
   (void)hipEventDestroy(a);
   (void)hipEventDestroy(b);
   dfree(sink);
-  const double chains = which == 2 ? 4.0 : 8.0;
-  const double per_op = which == 1 ? 2.0 : 1.0;  // FMA = 2 flops
-  *per_second = 4.0 * blocks * 256.0 * iters * chains * per_op / (ms * 1e-3);
+  // results per thread-iteration: exp / FMA chains, erf chains, LSE pairs
+  // (4 candidates x 8 components), quantized pairs (2 chains)
+  static const double per_iter[5] = {8.0, 16.0, 4.0, 32.0, 2.0};
+  *per_second = 4.0 * blocks * 256.0 * iters * per_iter[which] / (ms * 1e-3);
   return TPE_OK;
 }
 

@@ -674,29 +674,7 @@ __device__ void prep_slot(const tpe_hp &H, int64_t slot, int K, const double *w,
   }
   STAMP(8);
   const bool quant = (H.flags & TPE_HAS_Q) != 0;
-  const double L2E = 1.4426950408889634;  // log2(e)
-  const double A0 = sqrt(0.5 * L2E);
-  for (int k = threadIdx.x; k < K; k += blockDim.x) {
-    Coef c;
-    const double s = sg[k];
-    const double sp = np_maximum(s, kEPS);
-    c.x = mu[k];
-    c.w = 0.0;
-    if (quant) {
-      c.y = 1.0 / np_maximum(1.4142135623730951 * s, kEPS);
-      c.z = w[k];
-    } else if (H.family == TPE_GMM) {
-      // log(w / sqrt(2 pi sigma^2) / p_accept), tpe.py:140-144
-      const double Z = sqrt(2.0 * 3.141592653589793 * (s * s));
-      c.y = A0 / sp;
-      c.z = L2E * log(w[k] / Z / pacc);
-    } else {
-      // lognormal_lpdf + log w, minus log(x) per candidate, tpe.py:193-202, 280
-      c.y = A0 / sp;
-      c.z = L2E * (log(w[k]) - log(sp * 2.5066282746310002));
-    }
-    cf[k] = c;
-  }
+  for (int k = threadIdx.x; k < K; k += blockDim.x) cf[k] = make_coef(H, w[k], mu[k], sg[k], pacc);
   if (threadIdx.x == 0) {
     MixInfo mi;
     mi.K = K; mi.kind = quant ? 1 : 0; mi.p_accept = pacc; mi.log_pacc = log(pacc);
@@ -795,29 +773,10 @@ __device__ void fit_continuous(const FitArgs &A, const FitCtx &C, FitShared &sm,
   const double wsum = sums[0], pacc = sums[1];
   // per-component lpdf constants (tpe.py:138-160, 277-299) + copy-out
   const bool quant = (H.flags & TPE_HAS_Q) != 0;
-  const double L2E = 1.4426950408889634;  // log2(e)
-  const double A0 = sqrt(0.5 * L2E);
   Coef *cf = A.coef + slot * A.kcap;
   for (int k = threadIdx.x; k < K; k += blockDim.x) {
     const double s = sg[k], wk = w[k], mk = mu[k];
-    const double sp = np_maximum(s, kEPS);
-    Coef c;
-    c.x = mk;
-    c.w = 0.0;
-    if (quant) {
-      c.y = 1.0 / np_maximum(1.4142135623730951 * s, kEPS);
-      c.z = wk;
-    } else if (H.family == TPE_GMM) {
-      // log(w / sqrt(2 pi sigma^2) / p_accept), tpe.py:140-144
-      const double Z = sqrt(2.0 * 3.141592653589793 * (s * s));
-      c.y = A0 / sp;
-      c.z = L2E * log(wk / Z / pacc);
-    } else {
-      // lognormal_lpdf + log w, minus log(x) per candidate, tpe.py:193-202, 280
-      c.y = A0 / sp;
-      c.z = L2E * (log(wk) - log(sp * 2.5066282746310002));
-    }
-    cf[k] = c;
+    cf[k] = make_coef(H, wk, mk, s, pacc);
     if (MIXLDS) { gw[k] = wk; gm[k] = mk; gs[k] = s; }
   }
   if (threadIdx.x == 0) {

@@ -66,8 +66,8 @@ struct ScoreArgs {
   const int32_t *cand_pos;   // optional: original position of each (sorted) candidate
   double *out_lb, *out_la;   // optional per-candidate lliks (ext only)
   Partial *results;          // [S][P]
-  Partial *partial;          // [S][P][pstride] block argmax records
-  uint32_t *ticket;          // [S][P] arrival counters (zero between launches)
+  Partial *partial;          // [S][P][pstride] candidate-tile argmax records
+  uint32_t *ticket;          // [S][P] tile arrival counters (zero between launches)
   int64_t kcap;
   int64_t n_cand;
   int64_t cand_begin;
@@ -75,12 +75,12 @@ struct ScoreArgs {
   int32_t cand_slot0;        // slot of blockIdx.y == 0 within the candidate buffer
   int32_t pstride;           // partial records per (s, hp)
   int32_t n_hp;
-  int32_t n_slots;
-  int32_t ks;                // waves of a 16-wave block sharing 64 candidates
+  int32_t n_slots;            // hps of this launch (grid.y)
   int32_t tiles;             // candidate tiles per (s, hp)
   int32_t n_suggest;         // grid.z
   int32_t force_active;      // ignore conditions (operator-level scoring)
   int32_t accumulate;        // merge with results of an earlier candidate chunk
+  unsigned long long *census;  // optional [3]: quantized pairs total / live / executed
 };
 
 // Arguments of the fit kernels (tpe_fit.hip), one block per (hp, side) slot.
@@ -111,13 +111,10 @@ hipError_t launch_prep(const tpe_hp *hps, int32_t n_hp, const double *mw,
                        const double *mmu, const double *msig, MixInfo *info,
                        Coef *coef, int64_t kcap, double *scratch,
                        hipStream_t st);
-hipError_t launch_score(const ScoreArgs &a, int32_t kind, int32_t grid_x, hipStream_t st);
+constexpr int kTile = 64;  // candidates per scoring block (one per lane)
+hipError_t launch_score(const ScoreArgs &a, bool has_erf, hipStream_t st);
 hipError_t launch_draw(const ScoreArgs &a, hipStream_t st);
 hipError_t launch_bucket(const ScoreArgs &a, int32_t *pos_out, hipStream_t st);
-hipError_t launch_reduce(const int32_t *level_hps, int32_t n_slots,
-                         int32_t n_suggest, int32_t n_hp, int32_t grid_x,
-                         int32_t accumulate, const Partial *partial,
-                         Partial *results, hipStream_t st);
 hipError_t launch_merge(const int32_t *level_hps, int32_t n_slots,
                         int32_t n_suggest, int32_t n_hp, int32_t world,
                         const Partial *gathered, Partial *results,

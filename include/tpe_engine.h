@@ -196,16 +196,27 @@ int tpe_plan_score_candidates(tpe_plan_t p, int32_t hp, const double *x,
  * they evaluated.                                                          */
 int tpe_plan_last_stats(tpe_plan_t p, double *score_ms, double *pairs);
 
-/* Per-kernel profiling: record HIP events around every scoring launch of the
- * next `capacity` launches per lpdf kind (0: off), then read the average
- * device duration and the (candidate, component) pairs per launch of one
- * kind (0 LSE-GMM, 1 LSE-LGMM, 2 ERF-GMM, 3 ERF-LGMM, 4 categorical).     */
+/* Per-kernel profiling: record HIP events around each of the next `capacity`
+ * scoring launches (one per level and candidate chunk; every lpdf kind of the
+ * level), then read their average device duration and, for one lpdf kind
+ * (0 LSE-GMM, 1 LSE-LGMM, 2 ERF-GMM, 3 ERF-LGMM, 4 categorical), the
+ * (candidate, component) pairs per launch of that kind's active hps.
+ * tpe_plan_profile also clears the ring (capacity 0: off).                  */
 int tpe_plan_profile(tpe_plan_t p, int32_t capacity);
 int tpe_plan_profile_read(tpe_plan_t p, int32_t kind, double *avg_ms,
                           int64_t *launches, double *pairs_per_launch);
 
+/* Roofline accounting: read (counts may be NULL) and clear the census of the
+ * quantized-kind scoring work since the last call -- counts[0] valid
+ * (candidate, component) pairs, [1] live pairs (not an exact zero), [2]
+ * pairs evaluated (live for some lane of their wave) -- and switch the
+ * census on (enable != 0) or off for the following suggests.               */
+int tpe_plan_census(tpe_plan_t p, int32_t enable, int64_t *counts);
+
 /* Register-only microbenchmarks for the roofline: which = 0 v_exp_f32
- * (results/s), 1 fp64 FMA (flop/s), 2 OCML fp64 erf (results/s).          */
+ * (results/s), 1 fp64 FMA (flop/s), 2 OCML fp64 erf (results/s), 3 the
+ * log-sum-exp (candidate, component) pair of the scoring kernel (pairs/s),
+ * 4 a live quantized pair (2 fp64 erf; pairs/s).                           */
 int tpe_microbench(tpe_handle_t h, int32_t which, double *per_second);
 
 #ifdef __cplusplus

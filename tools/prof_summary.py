@@ -23,9 +23,8 @@ KIND = {0: 'lse_gmm', 1: 'lse_lgmm', 2: 'erf_gmm', 3: 'erf_lgmm', 4: 'categorica
 
 
 def short(name):
-    m = re.search(r'k_score<(\d)>', name)
-    if m:
-        return 'k_score<%s>' % KIND[int(m.group(1))]
+    if 'k_score' in name:
+        return 'k_score'
     m = re.search(r'(k_\w+(?:<\d>)?)', name)
     return m.group(1) if m else name.split('(')[0]
 
@@ -62,8 +61,8 @@ def main(src, tag, config):
         json.dump(summary, f, indent=1, sort_keys=True)
     tpath = os.path.join(out, 'traffic.json')
     traffic = json.load(open(tpath)) if os.path.exists(tpath) else {}
-    traffic[config] = {k[len('k_score<'):-1]: v['hbm_bytes'] for k, v in summary.items()
-                       if k.startswith('k_score<') and 'hbm_bytes' in v}
+    traffic[config] = {'score': v['hbm_bytes'] for k, v in summary.items()
+                       if k == 'k_score' and 'hbm_bytes' in v}
     traffic[config]['_source'] = '%s_%s_pmc.json (2*FETCH_SIZE+WRITE_SIZE KiB per launch)' % (
         tag, config)
     with open(tpath, 'w') as f:
