@@ -92,9 +92,11 @@ __device__ __forceinline__ Coef make_coef(const tpe_hp &H, double w, double mu, 
   c.w = 0.0;
   const double sp = np_maximum(sigma, kEPS);
   if (H.flags & TPE_HAS_Q) {
+    const double s2 = np_maximum(1.4142135623730951 * sigma, kEPS);
     c.x = mu;
-    c.y = 1.0 / np_maximum(1.4142135623730951 * sigma, kEPS);
+    c.y = 1.0 / s2;
     c.z = w;
+    c.w = 6.6 * s2;  // dead-zone half-width for the chunk test (tpe_score.hip)
     return c;
   }
   const double L2E = 1.4426950408889634;  // log2(e)

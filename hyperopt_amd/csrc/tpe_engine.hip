@@ -184,7 +184,9 @@ int compute_levels(tpe_engine *h, tpe_plan *p) {
     nl = std::max(nl, lev[i] + 1);
   }
   p->levels.assign(nl, {});
-  for (int kind = 0; kind <= KIND_CAT; ++kind)
+  // heaviest lpdf kind first: the scoring grid's low slots are dispatched
+  // first, so the long quantized tiles do not form the launch's tail
+  for (int kind : {KIND_ERF_L, KIND_ERF_G, KIND_LSE_L, KIND_LSE_G, KIND_CAT})
     for (int i = 0; i < p->P; ++i)
       if (score_kind(p->hps[i]) == kind) p->levels[lev[i]].push_back(i);
   p->level_off.assign(nl + 1, 0);
@@ -306,12 +308,40 @@ int ensure_ext(tpe_engine *h, tpe_plan *p, size_t n) {
   return TPE_OK;
 }
 
-// Scoring launch geometry: one 16-wave block per 64-candidate tile.
-struct Geom {
-  int32_t tiles;
-};
-Geom score_geometry(int64_t n_cand) {
-  return Geom{(int32_t)std::max<int64_t>(0, (n_cand + kTile - 1) / kTile)};
+// Scoring grid of one launch over n_slots slots whose lpdf kinds are `kinds`
+// (consecutive slots of one kind form a group, tiles of 64 * tile_rows(kind)
+// candidates).  Returns the partial-record stride (max tiles per slot), or -1
+// when the slots are not grouped by kind.
+int32_t set_score_groups(ScoreArgs &a, const int *kinds, int n_slots, int64_t cn) {
+  a.n_groups = 0;
+  int32_t blocks = 0, pstride = 1;
+  for (int j = 0; j < n_slots;) {
+    int k = j;
+    while (k < n_slots && kinds[k] == kinds[j]) ++k;
+    if (a.n_groups == kMaxGroups) return -1;
+    const int g = a.n_groups++;
+    const int64_t tc = 64 * tile_rows(kinds[j]);
+    const int32_t nt = (int32_t)((std::max<int64_t>(cn, 0) + tc - 1) / tc);
+    a.grp_kind[g] = kinds[j];
+    a.grp_slot0[g] = j;
+    a.grp_tiles[g] = nt;
+    a.grp_block0[g] = blocks;
+    blocks += nt * (k - j);
+    pstride = std::max(pstride, nt);
+    j = k;
+  }
+  a.grp_block0[a.n_groups] = blocks;
+  return pstride;
+}
+
+void copy_groups(ScoreArgs &a, const ScoreArgs &g) {
+  a.n_groups = g.n_groups;
+  for (int i = 0; i < kMaxGroups; ++i) {
+    a.grp_kind[i] = g.grp_kind[i];
+    a.grp_slot0[i] = g.grp_slot0[i];
+    a.grp_tiles[i] = g.grp_tiles[i];
+  }
+  for (int i = 0; i <= kMaxGroups; ++i) a.grp_block0[i] = g.grp_block0[i];
 }
 
 int ensure_cand(tpe_engine *h, tpe_plan *p, size_t n) {
@@ -404,8 +434,10 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
   const int32_t n_level = (int32_t)p->levels[level].size();
   const int32_t *lvl = p->d_level_hps + p->level_off[level];
   bool erf_level = false;
+  std::vector<int> kinds;
   for (int hp : p->levels[level]) {
     const int k = score_kind(p->hps[hp]);
+    kinds.push_back(k);
     erf_level |= k == KIND_ERF_G || k == KIND_ERF_L;
   }
   const int64_t budget = (int64_t)64 << 20;  // doubles
@@ -415,22 +447,25 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
   int64_t c0 = 0;
   do {
     const int64_t cn = std::min(chunk, n_cand - c0);
-    const Geom geo = score_geometry(cn);
-    int rc = ensure_suggest_state(h, p, n_sug, (size_t)n_sug * p->P * std::max(1, geo.tiles));
+    ScoreArgs grid{};
+    const int32_t pstride = set_score_groups(grid, kinds.data(), n_level, cn);
+    if (pstride < 0) return fail(h, TPE_E_INVALID, "level slots not grouped by lpdf kind");
+    int rc = ensure_suggest_state(h, p, n_sug, (size_t)n_sug * p->P * pstride);
     if (rc) return rc;
     rc = ensure_cand(h, p, (size_t)std::max<int64_t>(1, n_sug * n_level * cn));
     if (rc) return rc;
+    // buffers (re)allocated above: take their pointers only now
     ScoreArgs a = base_args(p, n_sug);
+    copy_groups(a, grid);
     a.cand = p->d_cand;
     a.cand_sstride = (int64_t)n_level * cn;
     a.n_cand = cn;
     a.cand_begin = cand_begin + c0;
-    a.pstride = std::max(1, geo.tiles);
+    a.pstride = pstride;
     a.accumulate = c0 > 0 ? 1 : 0;
     a.level_hps = lvl;
     a.n_slots = n_level;
     a.cand_slot0 = 0;
-    a.tiles = geo.tiles;
     for (int i = 0; i < kInlineSeeds && i < n_sug; ++i) a.seed_inline[i] = p->h_seeds[i];
     a.n_inline_seeds = (int32_t)std::min<int64_t>(n_sug, kInlineSeeds);
     CKH(launch_draw(a, st));
@@ -447,20 +482,21 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
 int run_external(tpe_engine *h, tpe_plan *p, int32_t hp, const double *ext, int64_t n,
                  double *lb, double *la, hipStream_t st) {
   const int kind = score_kind(p->hps[hp]);
-  const Geom geo = score_geometry(n);
-  int rc = ensure_suggest_state(h, p, 1, (size_t)p->P * std::max(1, geo.tiles));
+  ScoreArgs grid{};
+  const int32_t pstride = set_score_groups(grid, &kind, 1, n);
+  int rc = ensure_suggest_state(h, p, 1, (size_t)p->P * pstride);
   if (rc) return rc;
   ScoreArgs a = base_args(p, 1);
+  copy_groups(a, grid);
   a.cand = ext;
   a.cand_sstride = n;
   a.n_cand = n;
-  a.pstride = std::max(1, geo.tiles);
+  a.pstride = pstride;
   a.level_hps = p->d_all_hps + hp;
   a.n_slots = 1;
   a.out_lb = lb;
   a.out_la = la;
   a.force_active = 1;
-  a.tiles = geo.tiles;
   return score_launch(h, p, a, kind == KIND_ERF_G || kind == KIND_ERF_L, n, st, false);
 }
 

@@ -24,6 +24,12 @@ __host__ __device__ inline int score_kind(const tpe_hp &h) {
   return lg ? KIND_LSE_L : KIND_LSE_G;
 }
 
+// candidate rows (per lane) of a scoring tile of the kind: 64 * rows candidates
+__host__ __device__ constexpr int tile_rows(int kind) {
+  return (kind == KIND_ERF_G || kind == KIND_ERF_L) ? 1 : kind == KIND_CAT ? 4 : 2;
+}
+constexpr int kMaxGroups = 5;  // lpdf kinds: at most one group of each per launch
+
 struct MixInfo {
   int32_t K;        // components (categorical: upper)
   int32_t kind;     // 0 LSE, 1 ERF, 2 CAT
@@ -75,9 +81,14 @@ struct ScoreArgs {
   int32_t cand_slot0;        // slot of blockIdx.y == 0 within the candidate buffer
   int32_t pstride;           // partial records per (s, hp)
   int32_t n_hp;
-  int32_t n_slots;            // hps of this launch (grid.y)
-  int32_t tiles;             // candidate tiles per (s, hp)
-  int32_t n_suggest;         // grid.z
+  int32_t n_slots;            // hps of this launch
+  int32_t n_suggest;         // grid.y
+  // scoring grid: kind groups of consecutive slots (set_score_groups)
+  int32_t n_groups;
+  int32_t grp_kind[kMaxGroups];
+  int32_t grp_slot0[kMaxGroups];
+  int32_t grp_tiles[kMaxGroups];       // tiles per slot of the group
+  int32_t grp_block0[kMaxGroups + 1];  // first block of each group; [n_groups] = total
   int32_t force_active;      // ignore conditions (operator-level scoring)
   int32_t accumulate;        // merge with results of an earlier candidate chunk
   unsigned long long *census;  // optional [3]: quantized pairs total / live / executed
@@ -111,7 +122,6 @@ hipError_t launch_prep(const tpe_hp *hps, int32_t n_hp, const double *mw,
                        const double *mmu, const double *msig, MixInfo *info,
                        Coef *coef, int64_t kcap, double *scratch,
                        hipStream_t st);
-constexpr int kTile = 64;  // candidates per scoring block (one per lane)
 hipError_t launch_score(const ScoreArgs &a, bool has_erf, hipStream_t st);
 hipError_t launch_draw(const ScoreArgs &a, hipStream_t st);
 hipError_t launch_bucket(const ScoreArgs &a, int32_t *pos_out, hipStream_t st);

@@ -4,139 +4,265 @@
 //   GMM1_lpdf   tpe.py:104-166     LGMM1_lpdf  tpe.py:259-301
 //   categorical_lpdf tpe.py:50-57  broadcast_best tpe.py:749-759 (EI argmax)
 //
-// Work decomposition.  A block of 16 waves owns a tile of 64 candidates of
-// one (suggestion, hp): every wave holds the same 64 candidates, one per lane.
-// The components of both mixtures are staged in LDS (batches of 1024, 32 KB)
-// and wave w takes the components with index = w (mod 16) of each mixture,
-// reading them by broadcast, so a (candidate, component) pair costs only VALU
-// work, and the few live components of a quantized mixture (those near the
-// tile's candidates) are spread over all 16 waves.  Each wave reduces its
-// share per batch (log-sum-exp: a max pass and a sum pass; quantized: a
-// linear sum) and merges batches in order; then one wave per mixture merges
-// the 16 wave partials in wave order.  The reduction tree depends on (K_b,
-// K_a) only, so scores are bitwise independent of the grid, of candidate
-// chunking and of multi-GPU sharding.
+// Work decomposition.  A block of kWaves waves owns a tile of kTile = 64 * kR
+// candidates of one (suggestion, hp); every wave holds the same candidates,
+// kR per lane (candidate r * 64 + lane of the tile).  The components of both
+// mixtures are staged in LDS (batches of 1024, 32 KB) and wave w takes the
+// components with index = w (mod kWaves) of each mixture, reading each one by
+// broadcast once for its kR candidates, so a (candidate, component) pair costs
+// only VALU work, and the few live components of a quantized mixture (those
+// near the tile's value-sorted candidates) are spread over all waves.  Each
+// wave reduces its share per batch (log-sum-exp: a max pass and a sum pass;
+// quantized: a linear sum) and merges batches in order; then 2 * kR waves
+// (one per mixture and candidate row) merge the wave partials in wave order.
+// The reduction tree depends on (K_b, K_a) only, so scores are bitwise
+// independent of the grid, of candidate chunking and of multi-GPU sharding.
 //
 // Log-sum-exp (q = None): t = alpha + y'(beta + gamma y') (two fp64 FMAs, see
 // make_coef), 2^(t - max) with v_exp_f32 on the fp64 difference, fp64
 // accumulation.  Quantized: the reference's sum_k w (Phi(ub) - Phi(lb)) in
 // fp64 with OCML erf, in its operation order; a component whose two erf
 // arguments are beyond 6.5 on one side contributes an exact 0 and is skipped
-// when every lane of the wave agrees.
+// when every candidate of the wave agrees.
 #include <math.h>
 
 #include "tpe_device.hpp"
 
 namespace tpe {
 
-constexpr int kWaves = 16;     // waves per scoring block (all share the 64 candidates)
-constexpr int kStage = 1024;   // components staged in LDS per batch (32 KB)
+constexpr int kWaves = 8;       // waves per scoring block (all share the tile)
+constexpr int kRMax = 2;        // candidate rows (per lane) of the widest non-categorical tile
+constexpr int kChunk = 16;      // components per ownership chunk
+static_assert(2 * kRMax <= kWaves, "one merging wave per (mixture, candidate row)");
 
+// A log-sum-exp partial in log2 units: value = m + log2(s).  The exponent m
+// is kept integer-valued (or -inf), so every rescale of s to a new exponent is
+// an exact power-of-two ldexp; the only rounding is in the terms themselves.
 struct LseAcc {
-  double m, s;  // max and sum of 2^(t - m), log2 units
+  double m, s;
 };
 
 // merge b into a (a then b): the order every path uses
 __device__ __forceinline__ void lse_merge(LseAcc &a, const LseAcc &b) {
   if (b.m == -INFINITY && b.s == 0.0) return;
   if (a.m == -INFINITY && a.s == 0.0) { a = b; return; }
-  const bool nan = a.m != a.m || b.m != b.m;
-  const double M = nan ? NAN : fmax(a.m, b.m);
-  a.s = a.s * (double)__builtin_amdgcn_exp2f((float)(a.m - M)) +
-        b.s * (double)__builtin_amdgcn_exp2f((float)(b.m - M));
+  if (a.m != a.m || b.m != b.m) { a = LseAcc{NAN, NAN}; return; }
+  const double M = fmax(a.m, b.m);
+  a.s = ldexp(a.s, (int)fmax(a.m - M, -2100.0)) + ldexp(b.s, (int)fmax(b.m - M, -2100.0));
   a.m = M;
 }
 
-// the components i = first, first + st, ... < hi of an LDS batch, log-sum-exp:
-// a max pass and a sum pass (log2 units)
-__device__ __forceinline__ LseAcc lse_strided(const Coef *__restrict__ cs, int first, int hi,
-                                              int st, double y) {
-  double m = -INFINITY;
-  bool nan = y != y;
-#pragma unroll 4
-  for (int k = first; k < hi; k += st) {
-    const double cx = cs[k].x, cy = cs[k].y, cz = cs[k].z;
-    const double t = fma(fma(cz, y, cy), y, cx);
-    nan |= t != t;
-    m = fmax(m, t);
-  }
-  LseAcc r{m, 0.0};
-  if (nan) { r.m = NAN; r.s = NAN; return r; }
-  if (m == -INFINITY) return r;  // no terms, or every term -inf
-  double s = 0.0;
-#pragma unroll 4
-  for (int k = first; k < hi; k += st) {
-    const double cx = cs[k].x, cy = cs[k].y, cz = cs[k].z;
-    const double t = fma(fma(cz, y, cy), y, cx);
-    s += (double)__builtin_amdgcn_exp2f((float)(t - m));
-  }
-  r.s = s;
-  return r;
+// Coefficients read through the constant address space: the component loops
+// below index them with wave-uniform addresses, so they compile to scalar
+// loads (s_load into SGPRs, one per wave, no LDS or VGPR traffic per lane).
+typedef const Coef __attribute__((address_space(4))) KCoef;
+
+// a wave-uniform pointer as a scalar (the compiler cannot always prove it)
+__device__ __forceinline__ KCoef *uniform_ptr(const Coef *p) {
+  const uint64_t u = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  return (KCoef *)(((uint64_t)hi << 32) | lo);
 }
 
-// the same components, quantized: sum_k w (Phi(ub) - Phi(lb)),
-// tpe.py:146-160 (GMM: 0.5 * (1 + erf)) / 284-299 (LGMM: .5 + .5 * erf)
+// Component ownership: a mixture's components are cut into chunks of kChunk
+// consecutive indices and wave w owns the chunks c = w (mod kWaves), scanning
+// them in order; `c0` is the wave's first chunk.
+
+constexpr int kGroup = 8;  // components per scalar-load group (48 SGPRs)
+
+// Single-pass log-sum-exp over the wave's chunks of a mixture of nb
+// components against the lane's kR candidates (log2 units, t = alpha +
+// y'(beta + gamma y'), make_coef).  Per group of kGroup components: the group
+// max lifts the integer exponent m to ceil(max) if larger (exact ldexp rescale
+// of s), then s += 2^(t - m) with v_exp_f32 on the fp64 difference (every
+// term <= 1, the largest > 1/2).  A NaN term makes its 2^(t - m) NaN, which
+// reaches the lpdf as the reference's NaN (logsum_rows, tpe.py:37-40); fmax
+// drops it from the exponent, so a lane whose terms are all NaN keeps
+// m = -inf and scores NaN as well.
+template <int KR, bool TAIL>
+__device__ __forceinline__ void lse_group(KCoef *__restrict__ cs, int k, int k1,
+                                          const double (&y)[KR], double (&m)[KR],
+                                          double (&s)[KR]) {
+  double cx[kGroup], cy[kGroup], cz[kGroup];
+#pragma unroll
+  for (int j = 0; j < kGroup; ++j) {
+    const int kk = (TAIL && k + j >= k1) ? k : k + j;
+    cx[j] = cs[kk].x; cy[j] = cs[kk].y; cz[j] = cs[kk].z;
+  }
+#pragma unroll
+  for (int r = 0; r < KR; ++r) {
+    double t[kGroup], g = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < kGroup; ++j) {
+      t[j] = fma(fma(cz[j], y[r], cy[j]), y[r], cx[j]);
+      if (TAIL && k + j >= k1) t[j] = -INFINITY;  // wave-uniform
+      g = fmax(g, t[j]);
+    }
+    const double mn = fmax(m[r], ceil(g));
+    if (mn != m[r]) {  // s == 0 while m == -inf
+      s[r] = m[r] == -INFINITY ? s[r] : ldexp(s[r], (int)fmax(m[r] - mn, -2100.0));
+      m[r] = mn;
+    }
+    const double ms = mn == -INFINITY ? 0.0 : mn;  // all terms -inf / NaN so far
+#pragma unroll
+    for (int j = 0; j < kGroup; ++j)
+      s[r] += (double)__builtin_amdgcn_exp2f((float)(t[j] - ms));
+  }
+}
+
+template <int KR>
+__device__ __forceinline__ void lse_chunks(KCoef *__restrict__ cs, int c0, int nb,
+                                           const double (&y)[KR], LseAcc (&out)[KR]) {
+  double m[KR], s[KR];
+#pragma unroll
+  for (int r = 0; r < KR; ++r) { m[r] = -INFINITY; s[r] = 0.0; }
+  for (int c = c0; c * kChunk < nb; c += kWaves) {
+    const int k1 = min(nb, (c + 1) * kChunk);
+    int k = c * kChunk;
+    for (; k + kGroup <= k1; k += kGroup) lse_group<KR, false>(cs, k, k1, y, m, s);
+    if (k < k1) lse_group<KR, true>(cs, k, k1, y, m, s);
+  }
+#pragma unroll
+  for (int r = 0; r < KR; ++r) {
+    if (y[r] != y[r]) out[r] = LseAcc{NAN, NAN};
+    else if (m[r] == -INFINITY) out[r] = s[r] == 0.0 ? LseAcc{-INFINITY, 0.0} : LseAcc{NAN, NAN};
+    else out[r] = LseAcc{m[r], s[r]};
+  }
+}
+
 // CENSUS counts, per lane, the valid pairs, the live ones and the ones
-// evaluated (live for some lane of the wave) -- roofline accounting only.
+// evaluated (live for some candidate of the wave) -- roofline accounting only.
 struct Census {
   uint32_t total, live, exec;
 };
 
-template <bool LOGN, bool CENSUS>
-__device__ __forceinline__ double erf_strided(const Coef *__restrict__ cs, int first, int hi,
-                                              int st, double ub, double lb, bool valid,
-                                              Census &cen) {
+// the same chunks, quantized: sum_k w (Phi(ub) - Phi(lb)),
+// tpe.py:146-160 (GMM: 0.5 * (1 + erf)) / 284-299 (LGMM: .5 + .5 * erf).
+// A chunk is skipped when every candidate of the wave is provably beyond
+// 6.6 sigma-units of every one of its components on one side (Coef.w holds
+// 6.6 * max(sqrt(2) sigma, EPS)): all its terms are then exact zeros (erf
+// saturates to +-1 from 5.93).  wlo / whi: the wave's min lb / max ub;
+// `exact` false (a NaN bound) disables the chunk test.  Inside a chunk, a
+// component is skipped when all its terms in the wave are exact zeros.
+template <int KR, bool LOGN, bool CENSUS>
+__device__ __forceinline__ void erf_chunks(KCoef *__restrict__ cs, int c0, int nb,
+                                           const double (&ub)[KR], const double (&lb)[KR],
+                                           const bool (&valid)[KR], double wlo, double whi,
+                                           bool exact, double (&prob)[KR], Census &cen) {
 #pragma clang fp contract(off)
-  double prob = 0.0;
-  for (int k = first; k < hi; k += st) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int r = 0; r < KR; ++r) prob[r] = 0.0;
+  for (int c = c0; c * kChunk < nb; c += kWaves) {
+    const int k0 = c * kChunk, k1 = min(nb, k0 + kChunk);
+    if (exact) {  // the chunk's envelope, one component per lane of the first kChunk
+      double lo = INFINITY, hi = -INFINITY;
+      if (lane < k1 - k0) {
+        const double qx = cs[k0 + lane].x, qw = cs[k0 + lane].w;
+        lo = qx - qw;
+        hi = qx + qw;
+      }
+#pragma unroll
+      for (int o = kChunk / 2; o > 0; o >>= 1) {
+        lo = fmin(lo, __shfl_xor(lo, o, 64));
+        hi = fmax(hi, __shfl_xor(hi, o, 64));
+      }
+      lo = __shfl(lo, 0, 64);
+      hi = __shfl(hi, 0, 64);
+      if (wlo >= hi || whi <= lo) {
+        if constexpr (CENSUS) {
+#pragma unroll
+          for (int r = 0; r < KR; ++r) cen.total += valid[r] ? (uint32_t)(k1 - k0) : 0u;
+        }
+        continue;
+      }
+    }
+  for (int k = k0; k < k1; ++k) {
     const double cx = cs[k].x, cy = cs[k].y;
-    const double zu = (ub - cx) * cy;
-    const double zl = (lb - cx) * cy;
-    const bool dead = !valid || (zu >= 6.5 && zl >= 6.5) || (zu <= -6.5 && zl <= -6.5);
-    const bool skip = __all(dead);
+    double zu[KR], zl[KR];
+    bool dead_all = true;
+#pragma unroll
+    for (int r = 0; r < KR; ++r) {
+      zu[r] = (ub[r] - cx) * cy;
+      zl[r] = (lb[r] - cx) * cy;
+      const bool dead = !valid[r] || (zu[r] >= 6.5 && zl[r] >= 6.5) ||
+                        (zu[r] <= -6.5 && zl[r] <= -6.5);
+      dead_all &= dead;
+      if constexpr (CENSUS) {
+        cen.total += valid[r] ? 1u : 0u;
+        cen.live += dead ? 0u : 1u;
+      }
+    }
+    const bool skip = __all(dead_all);
     if constexpr (CENSUS) {
-      cen.total += valid ? 1u : 0u;
-      cen.live += dead ? 0u : 1u;
-      cen.exec += (valid && !skip) ? 1u : 0u;
+#pragma unroll
+      for (int r = 0; r < KR; ++r) cen.exec += (valid[r] && !skip) ? 1u : 0u;
     }
-    if (skip) continue;  // exact zeros for every lane of the wave
+    if (skip) continue;  // exact zeros for every candidate of the wave
     const double w = cs[k].z;
-    double cu, cl;
-    if (LOGN) {
-      cu = .5 + .5 * erf(zu);
-      cl = .5 + .5 * erf(zl);
-    } else {
-      cu = 0.5 * (1.0 + erf(zu));
-      cl = 0.5 * (1.0 + erf(zl));
+#pragma unroll
+    for (int r = 0; r < KR; ++r) {
+      double cu, cl;
+      if (LOGN) {
+        cu = .5 + .5 * erf(zu[r]);
+        cl = .5 + .5 * erf(zl[r]);
+      } else {
+        cu = 0.5 * (1.0 + erf(zu[r]));
+        cl = 0.5 * (1.0 + erf(zl[r]));
+      }
+      double inc = w * cu;
+      inc -= w * cl;
+      prob[r] += inc;
     }
-    double inc = w * cu;
-    inc -= w * cl;
-    prob += inc;
   }
-  return prob;
+  }
 }
 
+#ifdef TPE_STAMPS
+// diagnostic build only (make dbg; tools/score_stamps.py): per-block wall
+// clock (100 MHz) at entry, after the component loop and at the end, plus the
+// (slot, tile) and hardware ids of the block, for the blocks of suggestion 0
+__device__ unsigned long long g_score_stamps[8192][4];
+#define SSTAMP(i)                                                                        \
+  do {                                                                                   \
+    if (threadIdx.x == 0 && blockIdx.y == 0) {                                           \
+      const unsigned b = blockIdx.x & 8191;                                              \
+      g_score_stamps[b][i] = wall_clock64();                                             \
+      if (i == 0)                                                                        \
+        g_score_stamps[b][3] =                                                           \
+            ((unsigned long long)(slot & 0xffff) << 48) |                                \
+            ((unsigned long long)(tile & 0xffff) << 32) |                                \
+            ((unsigned long long)(__builtin_amdgcn_s_getreg(63488 | 20) & 0xf) << 16) |  \
+            (__builtin_amdgcn_s_getreg(63488 | 4) & 0xffff);                             \
+    }                                                                                    \
+  } while (0)
+#else
+#define SSTAMP(i) do {} while (0)
+#endif
+
 struct ScoreSmem {
-  Coef stage[kStage];              // 32 KB: one batch of components
-  double2 wpart[2][kWaves][64];    // 32 KB: per-wave partials (below, above)
+  double2 wpart[2][kWaves][kRMax][64];  // per-wave partials (below, above)
+  double2 merged[2][kRMax][64];         // merged per (mixture, candidate row)
 };
 
 template <int KIND, bool CENSUS>
-__device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm) {
+__device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, int slot, int tile,
+                                           int ntiles) {
+  constexpr int KR = tile_rows(KIND);
   constexpr bool LSE = KIND == KIND_LSE_G || KIND == KIND_LSE_L;
   constexpr bool ERF = KIND == KIND_ERF_G || KIND == KIND_ERF_L;
   constexpr bool CAT = KIND == KIND_CAT;
   constexpr bool LOGN = KIND == KIND_LSE_L || KIND == KIND_ERF_L;
-  Coef *stage = sm.stage;
-  auto &wpart = sm.wpart;
-  const int slot = blockIdx.y, s = blockIdx.z, tile = blockIdx.x;
+  const int s = blockIdx.y;
   const int hp = A.level_hps[slot];
   const tpe_hp H = A.hps[hp];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  SSTAMP(0);
   const bool act = A.force_active || hp_active(H, A.results + (int64_t)s * A.n_hp,
                                                   A.cond_parent, A.cond_branch);
   if (!act) {  // one record says "inactive"; no tickets are taken
-    if (blockIdx.x == 0 && threadIdx.x == 0)
+    if (tile == 0 && threadIdx.x == 0)
       A.results[(int64_t)s * A.n_hp + hp] = Partial{NAN, NAN, -1, 0, 0};
     return;
   }
@@ -148,58 +274,75 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm) {
   const double *__restrict__ cand = A.cand + coff;
   // only the quantized kinds' candidates are value-bucketed (k_bucket)
   const int32_t *__restrict__ cpos = (ERF && A.cand_pos) ? A.cand_pos + coff : nullptr;
-  const int64_t li = (int64_t)tile * 64 + lane;
-  const bool valid = li < A.n_cand;
-  const double x = valid ? cand[li] : (LOGN ? 1.0 : 0.0);
 
-  // candidate-side transforms, once per candidate
-  double y = 0.0, ub = 0.0, lb = 0.0;
-  if constexpr (LSE) {
-    y = (LOGN ? log(x) : x) - H.prior_mu;
-  } else if constexpr (ERF) {
-    const double hq = H.q / 2.0;
-    if constexpr (!LOGN) {
-      ub = (H.flags & TPE_HAS_HIGH) ? np_minimum(x + hq, H.high) : x + hq;
-      lb = (H.flags & TPE_HAS_LOW) ? np_maximum(x - hq, H.low) : x - hq;
-    } else {
-      const double u = (H.flags & TPE_HAS_HIGH) ? np_minimum(x + hq, exp(H.high)) : x + hq;
-      double l = (H.flags & TPE_HAS_LOW) ? np_maximum(x - hq, exp(H.low)) : x - hq;
-      l = np_maximum(0.0, l);
-      ub = u < 0.0 ? NAN : log(np_maximum(u, kEPS));
-      lb = log(np_maximum(l, kEPS));
+  int64_t li[KR];
+  bool valid[KR];
+  double x[KR], y[KR], ub[KR], lb[KR];
+#pragma unroll
+  for (int r = 0; r < KR; ++r) {
+    li[r] = (int64_t)tile * (64 * KR) + r * 64 + lane;
+    valid[r] = li[r] < A.n_cand;
+    x[r] = valid[r] ? cand[li[r]] : (LOGN ? 1.0 : 0.0);
+    y[r] = ub[r] = lb[r] = 0.0;
+    // candidate-side transforms, once per candidate
+    if constexpr (LSE) {
+      y[r] = (LOGN ? log(x[r]) : x[r]) - H.prior_mu;
+    } else if constexpr (ERF) {
+      const double hq = H.q / 2.0;
+      if constexpr (!LOGN) {
+        ub[r] = (H.flags & TPE_HAS_HIGH) ? np_minimum(x[r] + hq, H.high) : x[r] + hq;
+        lb[r] = (H.flags & TPE_HAS_LOW) ? np_maximum(x[r] - hq, H.low) : x[r] - hq;
+      } else {
+        const double u =
+            (H.flags & TPE_HAS_HIGH) ? np_minimum(x[r] + hq, exp(H.high)) : x[r] + hq;
+        double l = (H.flags & TPE_HAS_LOW) ? np_maximum(x[r] - hq, exp(H.low)) : x[r] - hq;
+        l = np_maximum(0.0, l);
+        ub[r] = u < 0.0 ? NAN : log(np_maximum(u, kEPS));
+        lb[r] = log(np_maximum(l, kEPS));
+      }
     }
   }
 
-  double2 res_b = make_double2(0.0, 0.0), res_a = res_b;  // lane's merged results (wave 0)
   if constexpr (!CAT) {
-    // components: below [0, Kb) then above [Kb, Kb + Ka), staged in batches
-    // of kStage; wave w owns the components of each mixture with index
-    // k = w (mod kWaves) -- live erf components spread over the waves
-    const int Kb = ib.K, Kt = ib.K + ia.K;
-    LseAcc lacc[2] = {{-INFINITY, 0.0}, {-INFINITY, 0.0}};
-    double pacc[2] = {0.0, 0.0};
-    Census cen{0u, 0u, 0u};
-    for (int b0 = 0; b0 < Kt; b0 += kStage) {
-      const int nb = min(kStage, Kt - b0);
-      __syncthreads();  // the previous batch is consumed
-      for (int i = threadIdx.x; i < nb; i += blockDim.x) {
-        const int k = b0 + i;
-        stage[i] = k < Kb ? cb[k] : ca[k - Kb];
-      }
-      __syncthreads();
+    // wave w owns the chunks c = w (mod kWaves) of each mixture (the live
+    // erf components of the tile spread over the waves)
+    LseAcc lacc[2][KR];
+    double pacc[2][KR];
 #pragma unroll
-      for (int mix = 0; mix < 2; ++mix) {
-        // this batch's part of mixture `mix`, in batch-local indices [lo, hi)
-        const int lo = max(0, (mix ? Kb : 0) - b0), hi = min(nb, (mix ? Kt : Kb) - b0);
-        if (lo >= hi) continue;
-        // first owned index >= lo: mixture-relative index = w (mod kWaves)
-        const int mbase = (mix ? Kb : 0) - b0;             // batch-local index of mixture k = 0
-        int first = lo + ((wave - (lo - mbase)) % kWaves + kWaves) % kWaves;
-        if constexpr (LSE) {
-          lse_merge(lacc[mix], lse_strided(stage, first, hi, kWaves, y));
-        } else {
-          pacc[mix] += erf_strided<LOGN, CENSUS>(stage, first, hi, kWaves, ub, lb, valid, cen);
-        }
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int r = 0; r < KR; ++r) { lacc[q][r] = LseAcc{-INFINITY, 0.0}; pacc[q][r] = 0.0; }
+    Census cen{0u, 0u, 0u};
+    // quantized: the wave's candidate envelope for the chunk skip test
+    double wlo = INFINITY, whi = -INFINITY;
+    bool exact = true;
+    if constexpr (ERF) {
+#pragma unroll
+      for (int r = 0; r < KR; ++r) {
+        if (!valid[r]) continue;
+        exact &= lb[r] == lb[r] && ub[r] == ub[r];
+        // both bounds: a clipped bound pair may come out with ub < lb
+        wlo = fmin(wlo, fmin(lb[r], ub[r]));
+        whi = fmax(whi, fmax(lb[r], ub[r]));
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        wlo = fmin(wlo, __shfl_xor(wlo, o, 64));
+        whi = fmax(whi, __shfl_xor(whi, o, 64));
+      }
+      exact = __all(exact);
+    }
+    // wave index as a scalar: the component addresses below are wave-uniform,
+    // so the coefficients come in through scalar loads (SGPR operands)
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+#pragma unroll
+    for (int mix = 0; mix < 2; ++mix) {
+      const Coef *__restrict__ cm = mix ? ca : cb;
+      const int K = mix ? ia.K : ib.K;
+      if constexpr (LSE) {
+        lse_chunks<KR>(uniform_ptr(cm), wv, K, y, lacc[mix]);
+      } else {
+        erf_chunks<KR, LOGN, CENSUS>(uniform_ptr(cm), wv, K, ub, lb, valid, wlo, whi, exact, pacc[mix], cen);
       }
     }
     if constexpr (CENSUS && ERF) {
@@ -211,61 +354,62 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm) {
         if (lane == 0) atomicAdd(A.census + q, c3[q]);
       }
     }
-    if constexpr (LSE) {
-      wpart[0][wave][lane] = make_double2(lacc[0].m, lacc[0].s);
-      wpart[1][wave][lane] = make_double2(lacc[1].m, lacc[1].s);
-    } else {
-      wpart[0][wave][lane] = make_double2(pacc[0], 0.0);
-      wpart[1][wave][lane] = make_double2(pacc[1], 0.0);
-    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int r = 0; r < KR; ++r)
+        sm.wpart[q][wave][r][lane] = LSE ? make_double2(lacc[q][r].m, lacc[q][r].s)
+                                         : make_double2(pacc[q][r], 0.0);
     __syncthreads();
-    // wave 0 merges the below partials, wave 1 the above ones, in wave order
-    double2 r = make_double2(0.0, 0.0);
-    if (wave < 2) {
-      r = wpart[wave][0][lane];
+    // wave 2r + q merges mixture q of candidate row r, in wave order
+    if (wave < 2 * KR) {
+      const int q = wave & 1, r = wave >> 1;
+      double2 v0 = sm.wpart[q][0][r][lane];
       for (int w = 1; w < kWaves; ++w) {
-        const double2 v = wpart[wave][w][lane];
+        const double2 v = sm.wpart[q][w][r][lane];
         if constexpr (LSE) {
-          LseAcc t{r.x, r.y};
+          LseAcc t{v0.x, v0.y};
           lse_merge(t, LseAcc{v.x, v.y});
-          r = make_double2(t.m, t.s);
+          v0 = make_double2(t.m, t.s);
         } else {
-          r.x += v.x;
+          v0.x += v.x;
         }
       }
-      if (wave == 1) wpart[1][1][lane] = r;  // slot already consumed by wave 1
+      sm.merged[q][r][lane] = v0;
     }
     __syncthreads();
-    res_b = r;
-    res_a = wpart[1][1][lane];
   }
+  SSTAMP(1);
   if (wave != 0) return;
 
   // ---- finalize the tile (wave 0): lpdfs, EI, argmax (numpy semantics)
   double best_s = NAN, best_v = NAN;
   int64_t best_i = -1;
-  if (valid) {
+#pragma unroll
+  for (int r = 0; r < KR; ++r) {
+    if (!valid[r]) continue;
     double lpb, lpa;
     if constexpr (LSE) {
       const double LN2 = 0.6931471805599453;
-      lpb = (res_b.x == -INFINITY) ? NAN : (res_b.x + log2(res_b.y)) * LN2;
-      lpa = (res_a.x == -INFINITY) ? NAN : (res_a.x + log2(res_a.y)) * LN2;
-      if constexpr (LOGN) { const double lx = log(x); lpb -= lx; lpa -= lx; }
+      const double2 b = sm.merged[0][r][lane], a = sm.merged[1][r][lane];
+      lpb = (b.x == -INFINITY) ? NAN : (b.x + log2(b.y)) * LN2;
+      lpa = (a.x == -INFINITY) ? NAN : (a.x + log2(a.y)) * LN2;
+      if constexpr (LOGN) { const double lx = log(x[r]); lpb -= lx; lpa -= lx; }
     } else if constexpr (ERF) {
-      lpb = log(res_b.x) - ib.log_pacc;
-      lpa = log(res_a.x) - ia.log_pacc;
+      lpb = log(sm.merged[0][r][lane].x) - ib.log_pacc;
+      lpa = log(sm.merged[1][r][lane].x) - ia.log_pacc;
     } else {
-      const int64_t c = (int64_t)x;
-      const bool in = (x >= 0.0) && (c < ib.K) && ((double)c == x);
+      const int64_t c = (int64_t)x[r];
+      const bool in = (x[r] >= 0.0) && (c < ib.K) && ((double)c == x[r]);
       lpb = in ? cb[c].x : NAN;
       lpa = in ? ca[c].x : NAN;
     }
-    const int64_t lo = cpos ? (int64_t)cpos[li] : li;  // original position
+    const int64_t lo = cpos ? (int64_t)cpos[li[r]] : li[r];  // original position
     if (A.out_lb) A.out_lb[lo] = lpb;
     if (A.out_la) A.out_la[lo] = lpa;
-    best_s = lpb - lpa;
-    best_v = x;
-    best_i = A.cand_begin + lo;
+    const double sc = lpb - lpa;
+    const int64_t gi = A.cand_begin + lo;
+    if (better(sc, gi, best_s, best_i)) { best_s = sc; best_v = x[r]; best_i = gi; }
   }
   wave_best(best_s, best_v, best_i);
   Partial *pbase = A.partial + ((int64_t)s * A.n_hp + hp) * A.pstride;
@@ -279,7 +423,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     uint32_t *tk = A.ticket + (int64_t)s * A.n_hp + hp;
     const uint32_t t = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    is_last = (t == (uint32_t)A.tiles - 1) ? 1 : 0;
+    is_last = (t == (uint32_t)ntiles - 1) ? 1 : 0;
     if (is_last) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -287,41 +431,58 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm) {
     }
   }
   is_last = __shfl(is_last, 0, 64);
+  SSTAMP(2);
   if (!is_last) return;
   double fs = NAN, fv = NAN;
   int64_t fi = -1;
-  for (int i = lane; i < A.tiles; i += 64) {
+  for (int i = lane; i < ntiles; i += 64) {
     const Partial q = pbase[i];
     if (better(q.score, q.index, fs, fi)) { fs = q.score; fv = q.value; fi = q.index; }
   }
   wave_best(fs, fv, fi);
   if (lane == 0) {
-    Partial *r = A.results + (int64_t)s * A.n_hp + hp;
-    if (!(A.accumulate && better(r->score, r->index, fs, fi))) *r = Partial{fs, fv, fi, 1, 0};
+    Partial *rr = A.results + (int64_t)s * A.n_hp + hp;
+    if (!(A.accumulate && better(rr->score, rr->index, fs, fi))) *rr = Partial{fs, fv, fi, 1, 0};
   }
 }
 
-// One launch scores every hp of a level (grid.y), each block dispatching on its
-// hp's lpdf kind, so log-sum-exp, quantized and categorical tiles share the
-// GPU without stream forks.  Without quantized hps the kernel is built for
-// <= 64 VGPRs (8 waves per SIMD); with them it keeps OCML erf's registers
-// (4 waves per SIMD) rather than spilling.
+#ifdef TPE_STAMPS
+}  // namespace tpe
+extern "C" int tpe_debug_score_stamps(unsigned long long *out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(tpe::g_score_stamps), sizeof(tpe::g_score_stamps)) ==
+                 hipSuccess ? 0 : -5;
+}
+namespace tpe {
+#endif
+
+// One launch scores every hp of a level: a 1-D grid of blocks over the
+// level's kind groups (ScoreArgs::grp_*), heaviest kind first, each group's
+// slots cut into tiles of 64 * tile_rows(kind) candidates (1 row for the
+// quantized kinds, whose per-pair cost is highest: smaller blocks spread their
+// work over more CUs; 2 for log-sum-exp; 4 for categorical lookups).
 template <bool ERFK, bool CENSUS>
-__global__ __launch_bounds__(kWaves * 64, ERFK ? 4 : 8) void k_score(ScoreArgs A) {
+__global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(4)))
+void k_score(ScoreArgs A) {
   __shared__ ScoreSmem sm;
-  const tpe_hp &H = A.hps[A.level_hps[blockIdx.y]];
-  switch (score_kind(H)) {
-    case KIND_LSE_G: score_tile<KIND_LSE_G, CENSUS>(A, sm); break;
-    case KIND_LSE_L: score_tile<KIND_LSE_L, CENSUS>(A, sm); break;
-    case KIND_ERF_G: if constexpr (ERFK) score_tile<KIND_ERF_G, CENSUS>(A, sm); break;
-    case KIND_ERF_L: if constexpr (ERFK) score_tile<KIND_ERF_L, CENSUS>(A, sm); break;
-    default: score_tile<KIND_CAT, CENSUS>(A, sm); break;
+  const int b = blockIdx.x;
+  int g = 0;
+  while (g + 1 < A.n_groups && b >= A.grp_block0[g + 1]) ++g;
+  const int local = b - A.grp_block0[g], nt = A.grp_tiles[g];
+  const int slot = A.grp_slot0[g] + local / nt, tile = local % nt;
+  switch (A.grp_kind[g]) {
+    case KIND_LSE_G: score_tile<KIND_LSE_G, CENSUS>(A, sm, slot, tile, nt); break;
+    case KIND_LSE_L: score_tile<KIND_LSE_L, CENSUS>(A, sm, slot, tile, nt); break;
+    case KIND_ERF_G: if constexpr (ERFK) score_tile<KIND_ERF_G, CENSUS>(A, sm, slot, tile, nt); break;
+    case KIND_ERF_L: if constexpr (ERFK) score_tile<KIND_ERF_L, CENSUS>(A, sm, slot, tile, nt); break;
+    default: score_tile<KIND_CAT, CENSUS>(A, sm, slot, tile, nt); break;
   }
 }
 
 hipError_t launch_score(const ScoreArgs &a, bool has_erf, hipStream_t st) {
-  if (a.n_slots <= 0 || a.n_suggest <= 0 || a.tiles <= 0) return hipSuccess;
-  const dim3 g((unsigned)a.tiles, a.n_slots, a.n_suggest);
+  if (a.n_groups <= 0 || a.n_suggest <= 0) return hipSuccess;
+  const int blocks = a.grp_block0[a.n_groups];
+  if (blocks <= 0) return hipSuccess;
+  const dim3 g((unsigned)blocks, a.n_suggest);
   if (has_erf) {
     if (a.census) k_score<true, true><<<g, kWaves * 64, 0, st>>>(a);
     else k_score<true, false><<<g, kWaves * 64, 0, st>>>(a);

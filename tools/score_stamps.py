@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Per-block timeline of the last k_score launch from the TPE_STAMPS
+diagnostic build (make -C hyperopt_amd/csrc dbg): for every block of
+suggestion 0, its start, the end of its component loop and its end (us from
+the launch's first block start), grouped by lpdf kind, plus the CU / XCD
+spread.  Diagnostic only; the product library has no stamps."""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ['TPE_ENGINE_LIB'] = os.path.join(ROOT, 'hyperopt_amd', 'libtpe_engine_dbg.so')
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+from hyperopt_amd import _engine as E  # noqa: E402
+
+
+def main(cfg, n_cand):
+    import torch
+    torch.cuda.set_device(0)
+    eng = E.Engine(0)
+    dom, losses, vals, active, nc = bench.build_workload(cfg)
+    n_cand = n_cand or nc
+    hps, conds, pprior = dom.space.engine_tables()
+    plan = E.Plan(eng, hps, conds, pprior, max_trials=losses.size)
+    plan.set_history(losses, vals, active)
+    for i in range(5):
+        plan.fit(gamma=0.25, prior_weight=1.0, lf=25)
+        plan.suggest([7 + i], n_cand, fetch=False)
+    eng.lib.tpe_synchronize(eng.h)
+    buf = (C.c_ulonglong * (8192 * 4))()
+    assert eng.lib.tpe_debug_score_stamps(buf) == 0
+    st = np.frombuffer(buf, dtype=np.uint64).reshape(8192, 4)
+    st = st.astype(np.int64)
+    nb = int((st[:, 0] > 0).sum())
+    t = st[:nb, :3]
+    rel = (t - t[:, 0].min()) / 100.0  # 100 MHz -> us
+    meta = st[:nb, 3]
+    slot = (meta >> 48) & 0xffff
+    tile = (meta >> 32) & 0xffff
+    xcc = (meta >> 16) & 0xf
+    cu = (meta >> 8) & 0xf
+    se = (meta >> 13) & 0x3
+    print('%s n_cand=%d blocks=%d; launch span %.1f us' % (cfg, n_cand, nb, rel[:, 2].max()))
+    for sl in np.unique(slot):
+        r = rel[slot == sl]
+        print('%2d tiles %3d  start %6.1f..%6.1f  loop %6.1f (max %6.1f)  tail %5.1f  end max %6.1f' %
+              (sl, (slot == sl).sum(), r[:, 0].min(), r[:, 0].max(), (r[:, 1] - r[:, 0]).mean(),
+               (r[:, 1] - r[:, 0]).max(), (r[:, 2] - r[:, 1]).mean(), r[:, 2].max()))
+    key = xcc * 64 + se * 16 + cu
+    u, c = np.unique(key, return_counts=True)
+    print('distinct (xcd, se, cu) ids: %d; blocks per id min/max %d/%d; per xcd %s' %
+          (u.size, c.min(), c.max(), np.bincount(xcc, minlength=8).tolist()))
+
+
+if __name__ == '__main__':
+    main(sys.argv[1] if len(sys.argv) > 1 else 'cfg2',
+         int(sys.argv[2]) if len(sys.argv) > 2 else 0)
