@@ -223,6 +223,8 @@ int plan_build(tpe_engine *h, const tpe_space *sp, int64_t max_trials, tpe_plan 
   int64_t kcap = p->ncap + 1;
   for (const auto &x : p->hps)
     if (x.family == TPE_CAT) kcap = std::max<int64_t>(kcap, x.upper);
+  // whole coefficient blocks per slot (coef_at, tpe_internal.hpp)
+  kcap = (kcap + kCoefBlock - 1) / kCoefBlock * kCoefBlock;
   p->kcap = kcap;
   for (const auto &x : p->hps) {
     const int k = score_kind(x);

@@ -655,7 +655,7 @@ __device__ void prep_slot(const tpe_hp &H, int64_t slot, int K, const double *w,
     for (int k = threadIdx.x; k < K; k += blockDim.x) {
       Coef c;
       c.x = log(w[k]); c.y = 0.0; c.z = 0.0; c.w = 0.0;
-      cf[k] = c;
+      store_coef(cf, k, c);
     }
     if (threadIdx.x == 0) {
       MixInfo mi;
@@ -674,7 +674,8 @@ __device__ void prep_slot(const tpe_hp &H, int64_t slot, int K, const double *w,
   }
   STAMP(8);
   const bool quant = (H.flags & TPE_HAS_Q) != 0;
-  for (int k = threadIdx.x; k < K; k += blockDim.x) cf[k] = make_coef(H, w[k], mu[k], sg[k], pacc);
+  for (int k = threadIdx.x; k < K; k += blockDim.x)
+    store_coef(cf, k, make_coef(H, w[k], mu[k], sg[k], pacc));
   if (threadIdx.x == 0) {
     MixInfo mi;
     mi.K = K; mi.kind = quant ? 1 : 0; mi.p_accept = pacc; mi.log_pacc = log(pacc);
@@ -776,7 +777,7 @@ __device__ void fit_continuous(const FitArgs &A, const FitCtx &C, FitShared &sm,
   Coef *cf = A.coef + slot * A.kcap;
   for (int k = threadIdx.x; k < K; k += blockDim.x) {
     const double s = sg[k], wk = w[k], mk = mu[k];
-    cf[k] = make_coef(H, wk, mk, s, pacc);
+    store_coef(cf, k, make_coef(H, wk, mk, s, pacc));
     if (MIXLDS) { gw[k] = wk; gm[k] = mk; gs[k] = s; }
   }
   if (threadIdx.x == 0) {

@@ -38,13 +38,29 @@ struct MixInfo {
   double wsum;      // sum of weights (sampler CDF total)
 };
 
-// Per-component scoring coefficients, 32 B (one s_load_dwordx8).
-//   LSE: x = mu, y = a (sqrt(.5 log2 e)/max(sigma,EPS)), z = c (log2 units)
-//   ERF: x = mu, y = 1/max(sqrt2*sigma, EPS), z = w
+// Per-component scoring coefficients (make_coef, tpe_device.hpp), 4 fields:
+//   LSE: x = alpha, y = beta, z = gamma (t = alpha + y'(beta + gamma y'))
+//   ERF: x = mu, y = 1/max(sqrt2*sigma, EPS), z = w, w = dead-zone half-width
 //   CAT: x = log p
+// A slot's table (kcap components, a multiple of kCoefBlock) is stored in
+// blocks of kCoefBlock components, field-major within a block
+// ([x0..x7][y0..y7][z0..z7][w0..w7], 256 B): a scoring wave fetches one
+// block's three log-sum-exp fields with three 64-B scalar loads.
 struct __attribute__((aligned(32))) Coef {
   double x, y, z, w;
 };
+constexpr int kCoefBlock = 8;
+// offset (in doubles) of field f (0..3 = x, y, z, w) of component k of a table
+__host__ __device__ constexpr int64_t coef_off(int64_t k, int f) {
+  return (k / kCoefBlock) * (4 * kCoefBlock) + f * kCoefBlock + (k % kCoefBlock);
+}
+__device__ __forceinline__ void store_coef(Coef *table, int64_t k, const Coef &c) {
+  double *t = reinterpret_cast<double *>(table);
+  t[coef_off(k, 0)] = c.x;
+  t[coef_off(k, 1)] = c.y;
+  t[coef_off(k, 2)] = c.z;
+  t[coef_off(k, 3)] = c.w;
+}
 
 struct Partial {  // == tpe_result layout
   double score;

@@ -55,24 +55,41 @@ __device__ __forceinline__ void lse_merge(LseAcc &a, const LseAcc &b) {
 // Coefficients read through the constant address space: the component loops
 // below index them with wave-uniform addresses, so they compile to scalar
 // loads (s_load into SGPRs, one per wave, no LDS or VGPR traffic per lane).
-typedef const Coef __attribute__((address_space(4))) KCoef;
+typedef const double __attribute__((address_space(4))) KDbl;
 
-// a wave-uniform pointer as a scalar (the compiler cannot always prove it)
-__device__ __forceinline__ KCoef *uniform_ptr(const Coef *p) {
+// a wave-uniform table pointer as a scalar (the compiler cannot always prove it)
+__device__ __forceinline__ KDbl *uniform_ptr(const Coef *p) {
   const uint64_t u = (uint64_t)p;
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
   const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
-  return (KCoef *)(((uint64_t)hi << 32) | lo);
+  return (KDbl *)(((uint64_t)hi << 32) | lo);
 }
 
 // Component ownership: a mixture's components are cut into chunks of kChunk
 // consecutive indices and wave w owns the chunks c = w (mod kWaves), scanning
 // them in order; `c0` is the wave's first chunk.
 
-constexpr int kGroup = 8;  // components per scalar-load group (48 SGPRs)
+constexpr int kGroup = kCoefBlock;  // components per scalar-load group: one table block
+static_assert(kChunk % kGroup == 0, "groups tile the chunks");
+
+struct CoefGroup {
+  double x[kGroup], y[kGroup], z[kGroup];
+};
+
+// three 64-B scalar loads: the x, y, z rows of the table block at k (whole
+// blocks are allocated, entries past the mixture are masked by the caller)
+__device__ __forceinline__ void load_group(KDbl *__restrict__ cs, int k, CoefGroup &g) {
+  KDbl *b = cs + coef_off(k, 0);
+#pragma unroll
+  for (int j = 0; j < kGroup; ++j) {
+    g.x[j] = b[j];
+    g.y[j] = b[kCoefBlock + j];
+    g.z[j] = b[2 * kCoefBlock + j];
+  }
+}
 
 // Single-pass log-sum-exp over the wave's chunks of a mixture of nb
-// components against the lane's kR candidates (log2 units, t = alpha +
+// components against the lane's KR candidates (log2 units, t = alpha +
 // y'(beta + gamma y'), make_coef).  Per group of kGroup components: the group
 // max lifts the integer exponent m to ceil(max) if larger (exact ldexp rescale
 // of s), then s += 2^(t - m) with v_exp_f32 on the fp64 difference (every
@@ -81,47 +98,57 @@ constexpr int kGroup = 8;  // components per scalar-load group (48 SGPRs)
 // drops it from the exponent, so a lane whose terms are all NaN keeps
 // m = -inf and scores NaN as well.
 template <int KR, bool TAIL>
-__device__ __forceinline__ void lse_group(KCoef *__restrict__ cs, int k, int k1,
+__device__ __forceinline__ void lse_group(const CoefGroup &g, int k, int nb,
                                           const double (&y)[KR], double (&m)[KR],
                                           double (&s)[KR]) {
-  double cx[kGroup], cy[kGroup], cz[kGroup];
-#pragma unroll
-  for (int j = 0; j < kGroup; ++j) {
-    const int kk = (TAIL && k + j >= k1) ? k : k + j;
-    cx[j] = cs[kk].x; cy[j] = cs[kk].y; cz[j] = cs[kk].z;
-  }
 #pragma unroll
   for (int r = 0; r < KR; ++r) {
-    double t[kGroup], g = -INFINITY;
+    double t[kGroup];
 #pragma unroll
     for (int j = 0; j < kGroup; ++j) {
-      t[j] = fma(fma(cz[j], y[r], cy[j]), y[r], cx[j]);
-      if (TAIL && k + j >= k1) t[j] = -INFINITY;  // wave-uniform
-      g = fmax(g, t[j]);
+      t[j] = fma(fma(g.z[j], y[r], g.y[j]), y[r], g.x[j]);
+      if (TAIL && k + j >= nb) t[j] = -INFINITY;  // wave-uniform
     }
-    const double mn = fmax(m[r], ceil(g));
-    if (mn != m[r]) {  // s == 0 while m == -inf
-      s[r] = m[r] == -INFINITY ? s[r] : ldexp(s[r], (int)fmax(m[r] - mn, -2100.0));
-      m[r] = mn;
-    }
-    const double ms = mn == -INFINITY ? 0.0 : mn;  // all terms -inf / NaN so far
+    // group max as a tree (fmax drops NaN terms)
+    double mx[kGroup];
 #pragma unroll
-    for (int j = 0; j < kGroup; ++j)
-      s[r] += (double)__builtin_amdgcn_exp2f((float)(t[j] - ms));
+    for (int j = 0; j < kGroup; ++j) mx[j] = t[j];
+#pragma unroll
+    for (int w = kGroup / 2; w > 0; w >>= 1)
+#pragma unroll
+      for (int j = 0; j < w; ++j) mx[j] = fmax(mx[j], mx[j + w]);
+    // lift the integer exponent; s == 0 while m == -inf, and the clamp turns
+    // the -inf / NaN differences of that state into a harmless ldexp of 0
+    const double mn = fmax(m[r], ceil(mx[0]));
+    s[r] = ldexp(s[r], (int)fmax(m[r] - mn, -2100.0));
+    m[r] = mn;
+    const double ms = mn == -INFINITY ? 0.0 : mn;  // all terms -inf / NaN so far
+    // terms 2^(t - m) <= 1 summed as an fp32 tree (<= kGroup), then in fp64
+    float e[kGroup];
+#pragma unroll
+    for (int j = 0; j < kGroup; ++j) e[j] = __builtin_amdgcn_exp2f((float)(t[j] - ms));
+#pragma unroll
+    for (int w = kGroup / 2; w > 0; w >>= 1)
+#pragma unroll
+      for (int j = 0; j < w; ++j) e[j] += e[j + w];
+    s[r] += (double)e[0];
   }
 }
 
 template <int KR>
-__device__ __forceinline__ void lse_chunks(KCoef *__restrict__ cs, int c0, int nb,
+__device__ __forceinline__ void lse_chunks(KDbl *__restrict__ cs, int c0, int nb,
                                            const double (&y)[KR], LseAcc (&out)[KR]) {
   double m[KR], s[KR];
 #pragma unroll
   for (int r = 0; r < KR; ++r) { m[r] = -INFINITY; s[r] = 0.0; }
   for (int c = c0; c * kChunk < nb; c += kWaves) {
     const int k1 = min(nb, (c + 1) * kChunk);
-    int k = c * kChunk;
-    for (; k + kGroup <= k1; k += kGroup) lse_group<KR, false>(cs, k, k1, y, m, s);
-    if (k < k1) lse_group<KR, true>(cs, k, k1, y, m, s);
+    for (int k = c * kChunk; k < k1; k += kGroup) {
+      CoefGroup g;
+      load_group(cs, k, g);
+      if (k + kGroup <= k1) lse_group<KR, false>(g, k, k1, y, m, s);
+      else lse_group<KR, true>(g, k, k1, y, m, s);
+    }
   }
 #pragma unroll
   for (int r = 0; r < KR; ++r) {
@@ -146,7 +173,7 @@ struct Census {
 // `exact` false (a NaN bound) disables the chunk test.  Inside a chunk, a
 // component is skipped when all its terms in the wave are exact zeros.
 template <int KR, bool LOGN, bool CENSUS>
-__device__ __forceinline__ void erf_chunks(KCoef *__restrict__ cs, int c0, int nb,
+__device__ __forceinline__ void erf_chunks(KDbl *__restrict__ cs, int c0, int nb,
                                            const double (&ub)[KR], const double (&lb)[KR],
                                            const bool (&valid)[KR], double wlo, double whi,
                                            bool exact, double (&prob)[KR], Census &cen) {
@@ -159,7 +186,7 @@ __device__ __forceinline__ void erf_chunks(KCoef *__restrict__ cs, int c0, int n
     if (exact) {  // the chunk's envelope, one component per lane of the first kChunk
       double lo = INFINITY, hi = -INFINITY;
       if (lane < k1 - k0) {
-        const double qx = cs[k0 + lane].x, qw = cs[k0 + lane].w;
+        const double qx = cs[coef_off(k0 + lane, 0)], qw = cs[coef_off(k0 + lane, 3)];
         lo = qx - qw;
         hi = qx + qw;
       }
@@ -179,7 +206,7 @@ __device__ __forceinline__ void erf_chunks(KCoef *__restrict__ cs, int c0, int n
       }
     }
   for (int k = k0; k < k1; ++k) {
-    const double cx = cs[k].x, cy = cs[k].y;
+    const double cx = cs[coef_off(k, 0)], cy = cs[coef_off(k, 1)];
     double zu[KR], zl[KR];
     bool dead_all = true;
 #pragma unroll
@@ -200,7 +227,7 @@ __device__ __forceinline__ void erf_chunks(KCoef *__restrict__ cs, int c0, int n
       for (int r = 0; r < KR; ++r) cen.exec += (valid[r] && !skip) ? 1u : 0u;
     }
     if (skip) continue;  // exact zeros for every candidate of the wave
-    const double w = cs[k].z;
+    const double w = cs[coef_off(k, 2)];
 #pragma unroll
     for (int r = 0; r < KR; ++r) {
       double cu, cl;
@@ -304,6 +331,17 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
   }
 
   if constexpr (!CAT) {
+    // warm this XCD's L2 with both mixtures' coefficient lines: one dword per
+    // 128-B line, issued before the component loop, so the loop's scalar loads
+    // hit L2 instead of each group paying a far (MALL / HBM) round trip
+    float sink = 0.f;
+    {
+      const int nlb = (ib.K + 3) >> 2, nla = (ia.K + 3) >> 2;
+      for (int i = threadIdx.x; i < nlb + nla; i += blockDim.x) {
+        const Coef *c = i < nlb ? cb + 4 * i : ca + 4 * (i - nlb);
+        sink += *(const volatile float *)c;
+      }
+    }
     // wave w owns the chunks c = w (mod kWaves) of each mixture (the live
     // erf components of the tile spread over the waves)
     LseAcc lacc[2][KR];
@@ -345,6 +383,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
         erf_chunks<KR, LOGN, CENSUS>(uniform_ptr(cm), wv, K, ub, lb, valid, wlo, whi, exact, pacc[mix], cen);
       }
     }
+    if (sink == 1.5e-30f) sm.merged[0][0][lane].y = sink;  // keeps the warm-up loads
     if constexpr (CENSUS && ERF) {
       unsigned long long c3[3] = {cen.total, cen.live, cen.exec};
 #pragma unroll
@@ -401,8 +440,8 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
     } else {
       const int64_t c = (int64_t)x[r];
       const bool in = (x[r] >= 0.0) && (c < ib.K) && ((double)c == x[r]);
-      lpb = in ? cb[c].x : NAN;
-      lpa = in ? ca[c].x : NAN;
+      lpb = in ? reinterpret_cast<const double *>(cb)[coef_off(c, 0)] : NAN;
+      lpa = in ? reinterpret_cast<const double *>(ca)[coef_off(c, 0)] : NAN;
     }
     const int64_t lo = cpos ? (int64_t)cpos[li[r]] : li[r];  // original position
     if (A.out_lb) A.out_lb[lo] = lpb;
@@ -461,7 +500,7 @@ namespace tpe {
 // quantized kinds, whose per-pair cost is highest: smaller blocks spread their
 // work over more CUs; 2 for log-sum-exp; 4 for categorical lookups).
 template <bool ERFK, bool CENSUS>
-__global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(4)))
+__global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(6)))
 void k_score(ScoreArgs A) {
   __shared__ ScoreSmem sm;
   const int b = blockIdx.x;

@@ -21,7 +21,13 @@ def main(cfg, n_cand):
     import torch
     torch.cuda.set_device(0)
     eng = E.Engine(0)
-    dom, losses, vals, active, nc = bench.build_workload(cfg)
+    if cfg.startswith('kind:'):  # one-kind space of tools/kind_bench.py
+        sys.path.insert(0, os.path.join(ROOT, 'tools'))
+        import kind_bench
+        dom, losses, vals, active = kind_bench.workload(cfg[5:])
+        nc = 4096
+    else:
+        dom, losses, vals, active, nc = bench.build_workload(cfg)
     n_cand = n_cand or nc
     hps, conds, pprior = dom.space.engine_tables()
     plan = E.Plan(eng, hps, conds, pprior, max_trials=losses.size)
