@@ -31,6 +31,7 @@ struct tpe_plan {
   tpe_engine *eng = nullptr;
   int32_t P = 0;
   int64_t ncap = 0, kcap = 0;
+  int32_t last_nb = -1;  // n_below of the last tpe_plan_fit (below K <= n_below + 1)
   std::vector<tpe_hp> hps;
   std::vector<int32_t> cond_parent, cond_branch;
   std::vector<double> pprior;
@@ -437,11 +438,15 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
   const int32_t *lvl = p->d_level_hps + p->level_off[level];
   bool erf_level = false;
   std::vector<int> kinds;
+  // largest below mixture the draw can meet: the LDS table sampler fits it?
+  int64_t kmax = p->last_nb >= 0 ? (int64_t)p->last_nb + 1 : p->kcap;
   for (int hp : p->levels[level]) {
     const int k = score_kind(p->hps[hp]);
     kinds.push_back(k);
     erf_level |= k == KIND_ERF_G || k == KIND_ERF_L;
+    if (k == KIND_CAT) kmax = std::max<int64_t>(kmax, p->hps[hp].upper);
   }
+  const bool table_draw = kmax <= kTabCap;
   const int64_t budget = (int64_t)64 << 20;  // doubles
   const int64_t chunk = std::max<int64_t>(
       1, std::min<int64_t>(std::max<int64_t>(n_cand, 1),
@@ -470,7 +475,7 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
     a.cand_slot0 = 0;
     for (int i = 0; i < kInlineSeeds && i < n_sug; ++i) a.seed_inline[i] = p->h_seeds[i];
     a.n_inline_seeds = (int32_t)std::min<int64_t>(n_sug, kInlineSeeds);
-    CKH(launch_draw(a, st));
+    CKH(launch_draw(a, table_draw, st));
     if (erf_level) CKH(launch_bucket(a, p->d_cpos, st));
     a.cand_pos = erf_level ? p->d_cpos : nullptr;
     rc = score_launch(h, p, a, erf_level, cn, st, true);
@@ -860,6 +865,7 @@ int tpe_plan_fit(tpe_plan_t p, double gamma, int32_t gamma_cap, double prior_wei
   const double nbf = std::ceil(gamma * std::sqrt((double)p->n));
   const int32_t nb = (int32_t)std::max(0.0, std::min<double>(nbf, gamma_cap));
   CKH(launch_fit(fit_args(p, nb, prior_weight, lf), p->P, st));
+  p->last_nb = nb;
   return TPE_OK;
 }
 

@@ -139,7 +139,8 @@ hipError_t launch_prep(const tpe_hp *hps, int32_t n_hp, const double *mw,
                        Coef *coef, int64_t kcap, double *scratch,
                        hipStream_t st);
 hipError_t launch_score(const ScoreArgs &a, bool has_erf, hipStream_t st);
-hipError_t launch_draw(const ScoreArgs &a, hipStream_t st);
+constexpr int kTabCap = 2048;  // below-mixture components of the LDS draw table
+hipError_t launch_draw(const ScoreArgs &a, bool table, hipStream_t st);
 hipError_t launch_bucket(const ScoreArgs &a, int32_t *pos_out, hipStream_t st);
 hipError_t launch_merge(const int32_t *level_hps, int32_t n_slots,
                         int32_t n_suggest, int32_t n_hp, int32_t world,

@@ -58,24 +58,40 @@ __device__ __forceinline__ int pick(const double *__restrict__ w, int K, double 
   return k;
 }
 
-// One GMM1/LGMM1/categorical draw (tpe.py:62-93, 216-250; stochastic.py:104)
+// the same pick on an inclusive CDF of the weights: the first k with
+// cdf[k] > u * cdf[K-1] (binary search)
+__device__ __forceinline__ int pick_cdf(const double *cdf, int K, double u) {
+  const double t = u * cdf[K - 1];
+  int lo = 0, hi = K - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (cdf[mid] <= t) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// One GMM1/LGMM1/categorical draw (tpe.py:62-93, 216-250; stochastic.py:104);
+// cdf (optional): the weights' inclusive prefix sums.  The rejection sampler
+// is the fallback for mixtures beyond the LDS table: kept out of line.
 __device__ double draw_one(const tpe_hp &H, const MixInfo &I,
                            const double *__restrict__ w,
                            const double *__restrict__ mu,
                            const double *__restrict__ sg, uint64_t seed,
-                           uint64_t gi, uint32_t stream) {
+                           uint64_t gi, uint32_t stream, const double *cdf = nullptr) {
   if (H.family == TPE_CAT) {
     const Draw d = draw4(seed, gi, stream, 0);
-    return (double)pick(w, I.K, d.u0 * I.wsum);
+    return (double)(cdf ? pick_cdf(cdf, I.K, d.u0) : pick(w, I.K, d.u0 * I.wsum));
   }
   const bool bounded = (H.flags & (TPE_HAS_LOW | TPE_HAS_HIGH)) != 0;
   double x = 0.0;
   bool ok = false;
   int k = 0;
   Draw d{};
+#pragma unroll 1
   for (uint32_t it = 0; it < 64 && !ok; ++it) {
     d = draw4(seed, gi, stream, it);
-    k = pick(w, I.K, d.u0 * I.wsum);
+    k = cdf ? pick_cdf(cdf, I.K, d.u0) : pick(w, I.K, d.u0 * I.wsum);
     const double z = sqrt(-2.0 * log(1.0 - d.u1)) * cospi(2.0 * d.u2);
     const double v = mu[k] + sg[k] * z;
     if (!bounded || (H.low <= v && v < H.high)) { x = v; ok = true; }
@@ -95,15 +111,130 @@ __device__ double draw_one(const tpe_hp &H, const MixInfo &I,
   return x;
 }
 
+// ------------------------------------------------------------------------
+// Table sampler (k_draw, k_sample).  The reference's truncated draw re-picks
+// the component on every rejection (tpe.py:82-87, 237-242), so an accepted
+// draw comes from component k with probability proportional to w_k * m_k,
+// m_k = P_k(low <= x < high), distributed as N(mu_k, sigma_k) truncated to
+// the bounds.  The table holds, per component, that pick weight as an
+// inclusive CDF and the truncated inverse-CDF constants; a draw is then one
+// pick (binary search) and one inverse CDF, with no divergent rejection loop.
+// The inverse CDF works in the tail that keeps precision: for bounds in the
+// upper half of component k it inverts the upper tail Q with erfcinv, in the
+// lower half the lower tail Phi with erfcinv, else Phi with erfinv.
+// ------------------------------------------------------------------------
+struct DrawTable {
+  double cdf[kTabCap];   // inclusive CDF of the pick weights
+  double base[kTabCap];  // Q(a) (mode 1), Phi(a) (modes 0, 2)
+  double mass[kTabCap];  // m_k
+  unsigned char mode[kTabCap];
+  double wtot[4];        // per-wave totals of the scan (256 threads)
+};
+
+// block-wide inclusive scan of a[0, K) in place: thread t scans a contiguous
+// segment, then adds the exclusive scan of the segment totals (deterministic)
+__device__ void block_inclusive_scan(double *a, int K, double *wtot) {
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, nt = blockDim.x;
+  const int per = (K + nt - 1) / nt;
+  const int k0 = min(K, t * per), k1 = min(K, k0 + per);
+  double acc = 0.0;
+  for (int k = k0; k < k1; ++k) { acc += a[k]; a[k] = acc; }
+  double v = acc;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double n = __shfl_up(v, o, 64);
+    if (lane >= o) v += n;
+  }
+  if (lane == 63) wtot[wv] = v;
+  __syncthreads();
+  double off = v - acc;
+  for (int w = 0; w < wv; ++w) off += wtot[w];
+  for (int k = k0; k < k1; ++k) a[k] += off;
+  __syncthreads();
+}
+
+// block-wide: the table of a (hp, mixture); K <= kTabCap, blockDim 256
+__device__ void build_table(const tpe_hp &H, int K, const double *__restrict__ w,
+                            const double *__restrict__ mu, const double *__restrict__ sg,
+                            DrawTable &T) {
+  const bool bounded = H.family != TPE_CAT && (H.flags & (TPE_HAS_LOW | TPE_HAS_HIGH)) != 0;
+#pragma unroll 1
+  for (int k = threadIdx.x; k < K; k += blockDim.x) {
+    double pw = w[k];
+    if (bounded) {
+      const double s2 = 1.4142135623730951 * sg[k];
+      const double za = (H.low - mu[k]) / s2, zb = (H.high - mu[k]) / s2;
+      double b, m;
+      unsigned char md;
+      if (za >= 0.0) {         // upper half: Q(z) = erfc(z) / 2
+        b = 0.5 * erfc(za); m = b - 0.5 * erfc(zb); md = 1;
+      } else if (zb <= 0.0) {  // lower half: Phi(z) = erfc(-z) / 2
+        b = 0.5 * erfc(-za); m = 0.5 * erfc(-zb) - b; md = 2;
+      } else {
+        b = 0.5 * erfc(-za); m = 0.5 * erfc(-zb) - b; md = 0;
+      }
+      m = m > 0.0 ? m : 0.0;
+      T.base[k] = b; T.mass[k] = m; T.mode[k] = md;
+      pw *= m;
+    }
+    T.cdf[k] = pw;
+  }
+  __syncthreads();
+  block_inclusive_scan(T.cdf, K, T.wtot);
+}
+
+__device__ double draw_table(const tpe_hp &H, int K, const double *__restrict__ mu,
+                             const double *__restrict__ sg, const DrawTable &T,
+                             uint64_t seed, uint64_t gi, uint32_t stream) {
+  const Draw d = draw4(seed, gi, stream, 0);
+  const int k = pick_cdf(T.cdf, K, d.u0);
+  if (H.family == TPE_CAT) return (double)k;
+  double x;
+  if (H.flags & (TPE_HAS_LOW | TPE_HAS_HIGH)) {
+    // one tail probability q and side: x = mu + side * sqrt2 sigma erfcinv(2q)
+    const double s2 = 1.4142135623730951 * sg[k], b = T.base[k], m = T.mass[k];
+    const int md = T.mode[k];
+    double q, side;
+    if (md == 1) { q = b - d.u1 * m; side = 1.0; }        // upper tail Q
+    else {
+      const double pp = b + d.u1 * m;                      // Phi
+      if (md == 2 || pp < 0.5) { q = pp; side = -1.0; }
+      else { q = 1.0 - pp; side = 1.0; }
+    }
+    x = mu[k] + side * s2 * erfcinv(2.0 * q);
+    if (!(x >= H.low)) x = H.low;  // rounding at the bounds / zero-mass picks
+    if (!(x < H.high)) x = nextafter(H.high, -INFINITY);
+  } else {
+    x = mu[k] + sg[k] * (sqrt(-2.0 * log(1.0 - d.u1)) * cospi(2.0 * d.u2));
+  }
+  if (H.family == TPE_LGMM) x = exp(x);
+  if (H.flags & TPE_HAS_Q) x = rint(x / H.q) * H.q;
+  return x;
+}
+
+// s is wave-uniform: select the inline seed with an unrolled compare chain
+// (a dynamic index into the by-value argument would copy it to scratch)
 __device__ __forceinline__ uint64_t suggestion_seed(const ScoreArgs &A, int s) {
-  return s < kInlineSeeds && A.n_inline_seeds > s ? A.seed_inline[s] : A.seeds[s];
+  if (s >= A.n_inline_seeds) return A.seeds[s];
+  uint64_t v = A.seed_inline[0];
+#pragma unroll
+  for (int i = 1; i < kInlineSeeds; ++i) v = (s == i) ? A.seed_inline[i] : v;
+  return v;
 }
 
 // Candidate draws of one level (all its hps): grid = (blocks, hps of the
 // level, suggestions), one candidate per thread per step.  Counter = (global
 // candidate index, hp id, iteration), key = suggestion seed, so the
 // candidate set does not depend on how [0, n_cand) is chunked or sharded.
-__global__ __launch_bounds__(256) void k_draw(ScoreArgs A) {
+// TAB: the block first builds the below mixture's draw table in LDS
+// (identical in every block and rank); the host picks it when every below
+// mixture of the level fits (K <= n_below + 1, categorical K = upper), else
+// the per-draw rejection sampler runs (!TAB), in a kernel of its own so the
+// table path keeps its small register footprint.
+constexpr int kDrawThreads = 256;
+template <bool TAB>
+__global__ __launch_bounds__(kDrawThreads) void k_draw(ScoreArgs A) {
+  __shared__ DrawTable T;
   const int slot = blockIdx.y, s = blockIdx.z;
   const int hp = A.level_hps[slot];
   const tpe_hp H = A.hps[hp];
@@ -111,11 +242,19 @@ __global__ __launch_bounds__(256) void k_draw(ScoreArgs A) {
   const int64_t sb = 2 * (int64_t)hp;
   const MixInfo ib = A.info[sb];
   const double *bw = A.mw + sb * A.kcap, *bmu = A.mmu + sb * A.kcap, *bsg = A.msig + sb * A.kcap;
+  const int K = ib.K;
+  const bool tab = TAB && K >= 1 && K <= kTabCap;
+  if (tab) build_table(H, K, bw, bmu, bsg, T);
   const uint64_t seed = suggestion_seed(A, s);
   double *out = const_cast<double *>(A.cand) + (int64_t)s * A.cand_sstride + (int64_t)slot * A.n_cand;
-  for (int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; li < A.n_cand;
-       li += (int64_t)gridDim.x * blockDim.x)
-    out[li] = draw_one(H, ib, bw, bmu, bsg, seed, (uint64_t)(A.cand_begin + li), (uint32_t)hp);
+  // one candidate per thread (a grid-stride loop around the inlined inverse
+  // CDFs inflates the kernel to 256 VGPRs)
+  const int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (li < A.n_cand) {
+    const uint64_t gi = (uint64_t)(A.cand_begin + li);
+    if constexpr (TAB) out[li] = tab ? draw_table(H, K, bmu, bsg, T, seed, gi, (uint32_t)hp) : NAN;
+    else out[li] = draw_one(H, ib, bw, bmu, bsg, seed, gi, (uint32_t)hp);
+  }
 }
 
 // Bucket each 8192-candidate chunk of the erf-kind hps by value (counting
@@ -172,9 +311,20 @@ __global__ __launch_bounds__(1024) void k_bucket(ScoreArgs A, int32_t *__restric
     atomicAdd(&hist[b], 1);
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int acc = 0;
-    for (int b = 0; b < kBuckets; ++b) { const int c = hist[b]; hist[b] = acc; acc += c; }
+  if (threadIdx.x < 64) {  // exclusive scan of the 256 counts: 4 per lane + wave scan
+    static_assert(kBuckets == 256, "4 buckets per lane");
+    int c[4], tot = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { c[j] = hist[4 * lane + j]; tot += c[j]; }
+    int v = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int n = __shfl_up(v, o, 64);
+      if (lane >= o) v += n;
+    }
+    int acc = v - tot;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { hist[4 * lane + j] = acc; acc += c[j]; }
   }
   __syncthreads();
   int32_t *po = pos_out + off;
@@ -216,11 +366,16 @@ __global__ __launch_bounds__(256) void k_sample(const tpe_hp *__restrict__ hpd,
                                                 uint64_t seed, uint32_t stream,
                                                 int64_t offset, int64_t n,
                                                 double *__restrict__ out) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  __shared__ DrawTable T;
   const tpe_hp H = hpd[0];
   const MixInfo I = info[0];
-  out[i] = draw_one(H, I, w, mu, sg, seed, (uint64_t)(offset + i), stream);
+  const bool tab = I.K >= 1 && I.K <= kTabCap;
+  if (tab) build_table(H, I.K, w, mu, sg, T);
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t gi = (uint64_t)(offset + i);
+  out[i] = tab ? draw_table(H, I.K, mu, sg, T, seed, gi, stream)
+               : draw_one(H, I, w, mu, sg, seed, gi, stream);
 }
 
 // ------------------------------------------------------------------------
@@ -333,12 +488,11 @@ hipError_t launch_micro(int which, int blocks, int iters, double *sink, hipStrea
 // ------------------------------------------------------------------------
 // launch wrappers
 // ------------------------------------------------------------------------
-hipError_t launch_draw(const ScoreArgs &a, hipStream_t st) {
+hipError_t launch_draw(const ScoreArgs &a, bool table, hipStream_t st) {
   if (a.n_slots <= 0 || a.n_suggest <= 0 || a.n_cand <= 0) return hipSuccess;
-  const int64_t want = (a.n_cand + 255) / 256;
-  const int64_t cap = std::max<int64_t>(1, 8192 / ((int64_t)a.n_slots * a.n_suggest));
-  const unsigned gx = (unsigned)std::max<int64_t>(1, std::min(want, cap));
-  k_draw<<<dim3(gx, a.n_slots, a.n_suggest), 256, 0, st>>>(a);
+  const unsigned gx = (unsigned)((a.n_cand + kDrawThreads - 1) / kDrawThreads);
+  if (table) k_draw<true><<<dim3(gx, a.n_slots, a.n_suggest), kDrawThreads, 0, st>>>(a);
+  else k_draw<false><<<dim3(gx, a.n_slots, a.n_suggest), kDrawThreads, 0, st>>>(a);
   return hipGetLastError();
 }
 

@@ -187,13 +187,15 @@ def _assert_near_tie(name, kw, trials, i, got, want):
 @pytest.mark.parametrize('name', domains.NAMES)
 def test_testopt_quality_device_philox(name):
     """The reference's quality thresholds with the default on-device Philox
-    stream, over 6 fmin seeds: the pass rate must be no worse than the
-    reference RandomState stream's on the same seeds (minus one run)."""
+    stream, over 16 fmin seeds: the pass rate must be no worse than the
+    reference RandomState stream's on the same seeds minus two runs (at 6
+    seeds one stream's 2-run dip is ordinary noise: tools/quality_rates.py
+    measured 14/16 vs 15/16 on branin, 15 vs 14 on quadratic1)."""
     kw, n = domains.settings(name)
     rates = {}
     for stream in ('philox', 'numpy'):
         wins = 0
-        for seed in range(6):
+        for seed in range(16):
             t = Trials()
             fmin(lambda x: x, domains.build(name, hp, H.scope, as_apply),
                  algo=functools.partial(tpe.suggest, rng_stream=stream, **kw), max_evals=n,
@@ -201,7 +203,7 @@ def test_testopt_quality_device_philox(name):
             assert len(t) == n
             wins += min(t.losses()) < domains.THRESH[name]
         rates[stream] = wins
-    assert rates['philox'] >= rates['numpy'] - 1 and rates['philox'] >= 3, rates
+    assert rates['philox'] >= rates['numpy'] - 2 and rates['philox'] >= 10, rates
 
 
 def test_philox_suggest_structure_and_determinism():
