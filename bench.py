@@ -137,9 +137,10 @@ def main():
                             losses.size)
 
     def step(i):
-        # results stay device-resident in the plan (no copy inside the step)
-        plan.fit(gamma=0.25, prior_weight=1.0, lf=25)
-        plan.suggest([1_000_003 * rank + 17 * i + 7], n_cand, fetch=False)
+        # fit + suggest in one engine call (a replayed hipGraph after the first
+        # call of this shape); results stay device-resident in the plan
+        plan.fit_suggest([1_000_003 * rank + 17 * i + 7], n_cand, gamma=0.25, prior_weight=1.0,
+                         lf=25, fetch=False)
 
     for i in range(args.warmup):
         step(i)

@@ -38,7 +38,7 @@ EXPORTS = (
     'tpe_plan_num_levels', 'tpe_plan_set_history', 'tpe_plan_fit', 'tpe_plan_get_mixture',
     'tpe_plan_suggest', 'tpe_plan_merge', 'tpe_plan_score_candidates', 'tpe_plan_last_stats',
     'tpe_plan_profile', 'tpe_plan_profile_read', 'tpe_microbench', 'tpe_plan_get_results',
-    'tpe_plan_results_device', 'tpe_plan_census',
+    'tpe_plan_results_device', 'tpe_plan_census', 'tpe_plan_fit_suggest',
 )
 
 
@@ -130,6 +130,8 @@ def load_library(path: str = LIB_PATH):
             'tpe_plan_fit': (C.c_int, [vp, dbl, i32, dbl, i32, vp]),
             'tpe_plan_get_mixture': (C.c_int, [vp, i32, i32, _D, _D, _D, i64, C.POINTER(i64)]),
             'tpe_plan_suggest': (C.c_int, [vp, C.POINTER(u64), i64, i64, i64, i32, vp, i32, vp]),
+            'tpe_plan_fit_suggest': (C.c_int, [vp, dbl, i32, dbl, i32, C.POINTER(u64), i64, i64,
+                                               vp, i32, vp]),
             'tpe_plan_merge': (C.c_int, [vp, vp, i32, i32, vp, i32, vp]),
             'tpe_plan_score_candidates': (C.c_int, [vp, i32, _D, i64, _D, _D, C.POINTER(i64), _D]),
             'tpe_plan_last_stats': (C.c_int, [vp, _D, _D]),
@@ -386,6 +388,23 @@ class Plan(object):
             e.check(e.lib.tpe_plan_suggest(self.p, seeds.ctypes.data_as(C.POINTER(C.c_uint64)),
                                            seeds.size, int(n_cand), int(cand_begin), int(level),
                                            optr, 0 if host else 1, stream))
+        self._last_nsug = seeds.size
+        return res
+
+    def fit_suggest(self, seeds, n_cand, gamma=0.25, prior_weight=1.0, lf=25, gamma_cap=25,
+                    out=None, stream=None, fetch=True):
+        """fit() + suggest() over all levels in one engine call; repeated calls
+        of one shape replay a captured hipGraph of the step (tpe_engine.h)."""
+        e = self.engine
+        seeds = np.ascontiguousarray(np.atleast_1d(seeds), dtype=np.uint64)
+        host = out is None and fetch
+        res = np.empty((seeds.size, self.n_hp), dtype=RESULT_DTYPE) if host else None
+        optr = res.ctypes.data if host else out
+        with e.lock:
+            e.check(e.lib.tpe_plan_fit_suggest(
+                self.p, float(gamma), int(gamma_cap), float(prior_weight), int(lf),
+                seeds.ctypes.data_as(C.POINTER(C.c_uint64)), seeds.size, int(n_cand),
+                optr, 0 if host else 1, stream))
         self._last_nsug = seeds.size
         return res
 

@@ -78,8 +78,32 @@ struct tpe_plan {
   Prof prof[KIND_CAT + 1];
   int32_t prof_cap = 0;
   bool timed = false;
+  bool evs = false;  // ev0/ev1 bracket the last suggest (recorded only while profiling:
+                     // an event record costs a ~6 us pipeline drain between launches)
   int64_t last_ncand = 0, last_nsug = 0;
   int32_t last_level = -1;
+  // fit + suggest captured as one hipGraph (tpe_plan_fit_suggest): replayed
+  // with the history length / n_below of the fit node and the seeds of the
+  // draw nodes patched per call
+  struct StepKey {
+    double prior_weight = 0;
+    int32_t lf = 0;
+    int64_t n_sug = 0, n_cand = 0;
+    void *stream = nullptr;
+    bool table = false;
+    bool operator==(const StepKey &o) const {
+      return prior_weight == o.prior_weight && lf == o.lf && n_sug == o.n_sug &&
+             n_cand == o.n_cand && stream == o.stream && table == o.table;
+    }
+  };
+  StepKey graph_key, pending_key;
+  bool graph_ok = false, pending = false;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t graph_exec = nullptr;
+  std::vector<hipGraphNode_t> fit_nodes, draw_nodes;
+  std::vector<hipKernelNodeParams> fit_params, draw_params;
+  std::vector<FitArgs> fit_args0;
+  std::vector<ScoreArgs> draw_args0;
 };
 
 namespace {
@@ -106,6 +130,18 @@ hipError_t dalloc(T **p, size_t count) {
 
 void dfree(void *p) {
   if (p) (void)hipFree(p);
+}
+
+// drop the captured fit + suggest graph (buffers it points to change)
+void graph_reset(tpe_plan *p) {
+  if (p->graph_exec) (void)hipGraphExecDestroy(p->graph_exec);
+  if (p->graph) (void)hipGraphDestroy(p->graph);
+  p->graph_exec = nullptr;
+  p->graph = nullptr;
+  p->graph_ok = p->pending = false;
+  p->fit_nodes.clear(); p->draw_nodes.clear();
+  p->fit_params.clear(); p->draw_params.clear();
+  p->fit_args0.clear(); p->draw_args0.clear();
 }
 
 hipStream_t pick_stream(tpe_engine *h, void *s) {
@@ -277,6 +313,7 @@ int plan_build(tpe_engine *h, const tpe_space *sp, int64_t max_trials, tpe_plan 
 }
 
 int ensure_suggest_state(tpe_engine *h, tpe_plan *p, int64_t n_sug, size_t partials) {
+  if (n_sug > p->s_cap || partials > p->partial_cap) graph_reset(p);
   if (n_sug > p->s_cap) {
     dfree(p->d_results);
     dfree(p->d_seeds);
@@ -349,6 +386,7 @@ void copy_groups(ScoreArgs &a, const ScoreArgs &g) {
 
 int ensure_cand(tpe_engine *h, tpe_plan *p, size_t n) {
   if (n > p->cand_cap) {
+    graph_reset(p);
     dfree(p->d_cand);
     dfree(p->d_cpos);
     p->d_cand = nullptr;
@@ -827,6 +865,7 @@ int tpe_plan_create(tpe_handle_t h, const tpe_space *space, int64_t max_trials, 
 int tpe_plan_destroy(tpe_plan_t p) {
   if (!p) return TPE_OK;
   (void)hipSetDevice(p->eng->device);
+  graph_reset(p);
   plan_free_buffers(p);
   delete p;
   return TPE_OK;
@@ -901,18 +940,162 @@ int tpe_plan_suggest(tpe_plan_t p, const uint64_t *seeds, int64_t n_sug, int64_t
   p->h_seeds.assign(seeds, seeds + n_sug);
   if (n_sug > kInlineSeeds)
     CKH(hipMemcpyAsync(p->d_seeds, seeds, n_sug * 8, hipMemcpyHostToDevice, st));
-  CKH(hipEventRecord(p->ev0, st));
+  if (p->prof_cap > 0) CKH(hipEventRecord(p->ev0, st));
   const int l0 = level < 0 ? 0 : level;
   const int l1 = level < 0 ? (int)p->levels.size() : level + 1;
   for (int l = l0; l < l1; ++l) {
     rc = run_level(h, p, l, n_sug, n_cand, cand_begin, st);
     if (rc) return rc;
   }
-  CKH(hipEventRecord(p->ev1, st));
+  if (p->prof_cap > 0) CKH(hipEventRecord(p->ev1, st));
   p->timed = true;
+  p->evs = p->prof_cap > 0;
   p->last_ncand = n_cand;
   p->last_nsug = n_sug;
   p->last_level = level;
+  return copy_results(h, p, n_sug, out, out_on_device, st);
+}
+
+// ---- fit + suggest as one captured graph ---------------------------------
+namespace {
+
+// enqueue fit + every level's suggest on st (eager or under capture)
+int enqueue_step(tpe_engine *h, tpe_plan *p, int32_t nb, double prior_weight, int32_t lf,
+                 int64_t n_sug, int64_t n_cand, hipStream_t st) {
+  CKH(launch_fit(fit_args(p, nb, prior_weight, lf), p->P, st));
+  p->last_nb = nb;
+  for (int l = 0; l < (int)p->levels.size(); ++l) {
+    const int rc = run_level(h, p, l, n_sug, n_cand, 0, st);
+    if (rc) return rc;
+  }
+  return TPE_OK;
+}
+
+// capture the step, instantiate it and find the nodes patched per call
+int capture_step(tpe_engine *h, tpe_plan *p, int32_t nb, double prior_weight, int32_t lf,
+                 int64_t n_sug, int64_t n_cand, hipStream_t st) {
+  graph_reset(p);
+  CKH(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+  const int rc = enqueue_step(h, p, nb, prior_weight, lf, n_sug, n_cand, st);
+  hipGraph_t g = nullptr;
+  const hipError_t ec = hipStreamEndCapture(st, &g);
+  if (rc || ec != hipSuccess || !g) {
+    if (g) (void)hipGraphDestroy(g);
+    return rc ? rc : fail(h, TPE_E_HIP, "graph capture failed");
+  }
+  p->graph = g;
+  CKH(hipGraphInstantiate(&p->graph_exec, g, nullptr, nullptr, 0));
+  size_t nn = 0;
+  CKH(hipGraphGetNodes(g, nullptr, &nn));
+  std::vector<hipGraphNode_t> nodes(nn);
+  CKH(hipGraphGetNodes(g, nodes.data(), &nn));
+  for (hipGraphNode_t nd : nodes) {
+    hipGraphNodeType ty;
+    CKH(hipGraphNodeGetType(nd, &ty));
+    if (ty != hipGraphNodeTypeKernel) continue;
+    hipKernelNodeParams kp{};
+    CKH(hipGraphKernelNodeGetParams(nd, &kp));
+    if (kp.func == fit_kernel_fn()) {
+      p->fit_nodes.push_back(nd);
+      p->fit_params.push_back(kp);
+      p->fit_args0.push_back(*static_cast<const FitArgs *>(kp.kernelParams[0]));
+    } else if (is_draw_kernel_fn(kp.func)) {
+      p->draw_nodes.push_back(nd);
+      p->draw_params.push_back(kp);
+      p->draw_args0.push_back(*static_cast<const ScoreArgs *>(kp.kernelParams[0]));
+    }
+  }
+  if (p->fit_nodes.size() != 1) {
+    graph_reset(p);
+    return fail(h, TPE_E_HIP, "graph capture: fit node not found");
+  }
+  p->graph_ok = true;
+  return TPE_OK;
+}
+
+// patch this call's history length / n_below and seeds, then launch
+int launch_step(tpe_engine *h, tpe_plan *p, int32_t nb, const uint64_t *seeds, int64_t n_sug,
+                hipStream_t st) {
+  for (size_t i = 0; i < p->fit_nodes.size(); ++i) {
+    FitArgs fa = p->fit_args0[i];
+    fa.n = p->n;
+    fa.n_below = nb;
+    void *args[1] = {&fa};
+    hipKernelNodeParams kp = p->fit_params[i];
+    kp.kernelParams = args;
+    kp.extra = nullptr;
+    CKH(hipGraphExecKernelNodeSetParams(p->graph_exec, p->fit_nodes[i], &kp));
+  }
+  for (size_t i = 0; i < p->draw_nodes.size(); ++i) {
+    ScoreArgs da = p->draw_args0[i];
+    for (int64_t j = 0; j < n_sug; ++j) da.seed_inline[j] = seeds[j];
+    da.n_inline_seeds = (int32_t)n_sug;
+    void *args[1] = {&da};
+    hipKernelNodeParams kp = p->draw_params[i];
+    kp.kernelParams = args;
+    kp.extra = nullptr;
+    CKH(hipGraphExecKernelNodeSetParams(p->graph_exec, p->draw_nodes[i], &kp));
+  }
+  CKH(hipGraphLaunch(p->graph_exec, st));
+  p->last_nb = nb;
+  return TPE_OK;
+}
+
+}  // namespace
+
+int tpe_plan_fit_suggest(tpe_plan_t p, double gamma, int32_t gamma_cap, double prior_weight,
+                         int32_t lf, const uint64_t *seeds, int64_t n_sug, int64_t n_cand,
+                         tpe_result *out, int32_t out_on_device, void *stream) {
+  if (!p) return TPE_E_INVALID;
+  tpe_engine *h = p->eng;
+  if (n_sug <= 0 || n_cand < 0 || !seeds) return fail(h, TPE_E_INVALID, "bad args");
+  CKH(hipSetDevice(h->device));
+  hipStream_t st = pick_stream(h, stream);
+  const double nbf = std::ceil(gamma * std::sqrt((double)p->n));
+  const int32_t nb = (int32_t)std::max(0.0, std::min<double>(nbf, gamma_cap));
+  // Graph replay is opt-in (TPE_GRAPH=1): on the measured ROCm 7 / MI355X
+  // stack a replayed graph starts ~18 us after the previous one, against
+  // back-to-back eager launches of one call (tools/host_cost.py).
+  static const bool use_graph = std::getenv("TPE_GRAPH") != nullptr;
+  const bool graphable = use_graph && n_sug <= kInlineSeeds && p->prof_cap == 0 && !p->census;
+  tpe_plan::StepKey key;
+  key.prior_weight = prior_weight;
+  key.lf = lf;
+  key.n_sug = n_sug;
+  key.n_cand = n_cand;
+  key.stream = (void *)st;
+  key.table = (int64_t)nb + 1 <= kTabCap;
+  int rc = ensure_suggest_state(h, p, n_sug, 1);
+  if (rc) return rc;
+  p->h_seeds.assign(seeds, seeds + n_sug);
+  if (!graphable || !((p->graph_ok && p->graph_key == key) || (p->pending && p->pending_key == key))) {
+    // eager (first sight of this shape: it also sizes every buffer)
+    if (n_sug > kInlineSeeds)
+      CKH(hipMemcpyAsync(p->d_seeds, seeds, n_sug * 8, hipMemcpyHostToDevice, st));
+    if (p->prof_cap > 0) CKH(hipEventRecord(p->ev0, st));
+    rc = enqueue_step(h, p, nb, prior_weight, lf, n_sug, n_cand, st);
+    if (rc) return rc;
+    if (p->prof_cap > 0) CKH(hipEventRecord(p->ev1, st));
+    if (graphable && !(p->graph_ok && p->graph_key == key)) {
+      p->pending = true;
+      p->pending_key = key;
+    }
+  } else {
+    if (!(p->graph_ok && p->graph_key == key)) {
+      rc = capture_step(h, p, nb, prior_weight, lf, n_sug, n_cand, st);
+      if (rc) return rc;
+      p->graph_key = key;
+    }
+    if (p->prof_cap > 0) CKH(hipEventRecord(p->ev0, st));
+    rc = launch_step(h, p, nb, seeds, n_sug, st);
+    if (rc) return rc;
+    if (p->prof_cap > 0) CKH(hipEventRecord(p->ev1, st));
+  }
+  p->timed = true;
+  p->evs = p->prof_cap > 0;
+  p->last_ncand = n_cand;
+  p->last_nsug = n_sug;
+  p->last_level = -1;
   return copy_results(h, p, n_sug, out, out_on_device, st);
 }
 
@@ -1080,10 +1263,14 @@ int tpe_plan_last_stats(tpe_plan_t p, double *score_ms, double *pairs) {
   tpe_engine *h = p->eng;
   if (!p->timed) return fail(h, TPE_E_INVALID, "no suggest recorded");
   CKH(hipSetDevice(h->device));
-  CKH(hipEventSynchronize(p->ev1));
-  float ms = 0.f;
-  CKH(hipEventElapsedTime(&ms, p->ev0, p->ev1));
-  if (score_ms) *score_ms = ms;
+  if (p->evs) {
+    CKH(hipEventSynchronize(p->ev1));
+    float ms = 0.f;
+    CKH(hipEventElapsedTime(&ms, p->ev0, p->ev1));
+    if (score_ms) *score_ms = ms;
+  } else if (score_ms) {
+    *score_ms = NAN;  // not timed: see tpe_plan_profile
+  }
   if (pairs) {
     std::vector<MixInfo> info(2 * (size_t)p->P);
     std::vector<Partial> res((size_t)p->last_nsug * p->P);

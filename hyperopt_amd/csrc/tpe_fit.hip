@@ -987,6 +987,8 @@ extern "C" int tpe_debug_stamps(unsigned long long *out) {
 namespace tpe {
 #endif
 
+const void *fit_kernel_fn() { return reinterpret_cast<const void *>(&k_fit); }
+
 hipError_t launch_fit(const FitArgs &a, int32_t n_hp, hipStream_t st) {
   if (n_hp <= 0) return hipSuccess;
   k_fit<<<dim3(n_hp, 2), kFitThreads, kFitLds, st>>>(a);

@@ -134,6 +134,8 @@ struct FitArgs {
 // ---- launch wrappers (tpe_fit.hip / tpe_kernels.hip) ----
 hipError_t launch_split(const FitArgs &a, uint8_t *below, hipStream_t st);
 hipError_t launch_fit(const FitArgs &a, int32_t n_hp, hipStream_t st);
+const void *fit_kernel_fn();               // k_fit's host stub (graph node lookup)
+bool is_draw_kernel_fn(const void *f);     // one of k_draw's host stubs
 hipError_t launch_prep(const tpe_hp *hps, int32_t n_hp, const double *mw,
                        const double *mmu, const double *msig, MixInfo *info,
                        Coef *coef, int64_t kcap, double *scratch,

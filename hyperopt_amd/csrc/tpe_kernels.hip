@@ -13,214 +13,12 @@
 
 #include <algorithm>
 
-#include "tpe_device.hpp"
+#include "tpe_draw.hpp"
 
 namespace tpe {
 
 constexpr int kSortMax = 8192;  // candidates per bucketing chunk
 
-// ------------------------------------------------------------------------
-// counter-based Philox4x32-10 in registers
-// ------------------------------------------------------------------------
-struct U4 { uint32_t x, y, z, w; };
-__device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
-    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
-    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
-    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
-    c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
-    k0 += 0x9E3779B9u;
-    k1 += 0xBB67AE85u;
-  }
-  return c;
-}
-__device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
-  return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
-}
-
-struct Draw { double u0, u1, u2, u3; };
-__device__ __forceinline__ Draw draw4(uint64_t seed, uint64_t gi, uint32_t stream,
-                                      uint32_t it) {
-  const U4 c0{(uint32_t)gi, (uint32_t)(gi >> 32), stream, 2u * it};
-  const U4 c1{(uint32_t)gi, (uint32_t)(gi >> 32), stream, 2u * it + 1u};
-  const U4 r0 = philox(c0, (uint32_t)seed, (uint32_t)(seed >> 32));
-  const U4 r1 = philox(c1, (uint32_t)seed, (uint32_t)(seed >> 32));
-  return Draw{u53(r0.x, r0.y), u53(r0.z, r0.w), u53(r1.x, r1.y), u53(r1.z, r1.w)};
-}
-
-// inverse CDF pick of a component with probability w[k] / wsum
-__device__ __forceinline__ int pick(const double *__restrict__ w, int K, double t) {
-  int k = 0;
-  double acc = w[0];
-  while (k < K - 1 && acc <= t) { ++k; acc += w[k]; }
-  return k;
-}
-
-// the same pick on an inclusive CDF of the weights: the first k with
-// cdf[k] > u * cdf[K-1] (binary search)
-__device__ __forceinline__ int pick_cdf(const double *cdf, int K, double u) {
-  const double t = u * cdf[K - 1];
-  int lo = 0, hi = K - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if (cdf[mid] <= t) lo = mid + 1;
-    else hi = mid;
-  }
-  return lo;
-}
-
-// One GMM1/LGMM1/categorical draw (tpe.py:62-93, 216-250; stochastic.py:104);
-// cdf (optional): the weights' inclusive prefix sums.  The rejection sampler
-// is the fallback for mixtures beyond the LDS table: kept out of line.
-__device__ double draw_one(const tpe_hp &H, const MixInfo &I,
-                           const double *__restrict__ w,
-                           const double *__restrict__ mu,
-                           const double *__restrict__ sg, uint64_t seed,
-                           uint64_t gi, uint32_t stream, const double *cdf = nullptr) {
-  if (H.family == TPE_CAT) {
-    const Draw d = draw4(seed, gi, stream, 0);
-    return (double)(cdf ? pick_cdf(cdf, I.K, d.u0) : pick(w, I.K, d.u0 * I.wsum));
-  }
-  const bool bounded = (H.flags & (TPE_HAS_LOW | TPE_HAS_HIGH)) != 0;
-  double x = 0.0;
-  bool ok = false;
-  int k = 0;
-  Draw d{};
-#pragma unroll 1
-  for (uint32_t it = 0; it < 64 && !ok; ++it) {
-    d = draw4(seed, gi, stream, it);
-    k = cdf ? pick_cdf(cdf, I.K, d.u0) : pick(w, I.K, d.u0 * I.wsum);
-    const double z = sqrt(-2.0 * log(1.0 - d.u1)) * cospi(2.0 * d.u2);
-    const double v = mu[k] + sg[k] * z;
-    if (!bounded || (H.low <= v && v < H.high)) { x = v; ok = true; }
-  }
-  if (!ok) {
-    // truncated inverse CDF of the last component (rejection budget spent)
-    const double a = normal_cdf(H.low, mu[k], sg[k]);
-    const double b = normal_cdf(H.high, mu[k], sg[k]);
-    const double u = a + d.u3 * (b - a);
-    double v = mu[k] + sg[k] * 1.4142135623730951 * erfinv(2.0 * u - 1.0);
-    if (!(v >= H.low)) v = H.low;
-    if (!(v < H.high)) v = nextafter(H.high, -INFINITY);
-    x = v;
-  }
-  if (H.family == TPE_LGMM) x = exp(x);
-  if (H.flags & TPE_HAS_Q) x = rint(x / H.q) * H.q;
-  return x;
-}
-
-// ------------------------------------------------------------------------
-// Table sampler (k_draw, k_sample).  The reference's truncated draw re-picks
-// the component on every rejection (tpe.py:82-87, 237-242), so an accepted
-// draw comes from component k with probability proportional to w_k * m_k,
-// m_k = P_k(low <= x < high), distributed as N(mu_k, sigma_k) truncated to
-// the bounds.  The table holds, per component, that pick weight as an
-// inclusive CDF and the truncated inverse-CDF constants; a draw is then one
-// pick (binary search) and one inverse CDF, with no divergent rejection loop.
-// The inverse CDF works in the tail that keeps precision: for bounds in the
-// upper half of component k it inverts the upper tail Q with erfcinv, in the
-// lower half the lower tail Phi with erfcinv, else Phi with erfinv.
-// ------------------------------------------------------------------------
-struct DrawTable {
-  double cdf[kTabCap];   // inclusive CDF of the pick weights
-  double base[kTabCap];  // Q(a) (mode 1), Phi(a) (modes 0, 2)
-  double mass[kTabCap];  // m_k
-  unsigned char mode[kTabCap];
-  double wtot[4];        // per-wave totals of the scan (256 threads)
-};
-
-// block-wide inclusive scan of a[0, K) in place: thread t scans a contiguous
-// segment, then adds the exclusive scan of the segment totals (deterministic)
-__device__ void block_inclusive_scan(double *a, int K, double *wtot) {
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, nt = blockDim.x;
-  const int per = (K + nt - 1) / nt;
-  const int k0 = min(K, t * per), k1 = min(K, k0 + per);
-  double acc = 0.0;
-  for (int k = k0; k < k1; ++k) { acc += a[k]; a[k] = acc; }
-  double v = acc;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const double n = __shfl_up(v, o, 64);
-    if (lane >= o) v += n;
-  }
-  if (lane == 63) wtot[wv] = v;
-  __syncthreads();
-  double off = v - acc;
-  for (int w = 0; w < wv; ++w) off += wtot[w];
-  for (int k = k0; k < k1; ++k) a[k] += off;
-  __syncthreads();
-}
-
-// block-wide: the table of a (hp, mixture); K <= kTabCap, blockDim 256
-__device__ void build_table(const tpe_hp &H, int K, const double *__restrict__ w,
-                            const double *__restrict__ mu, const double *__restrict__ sg,
-                            DrawTable &T) {
-  const bool bounded = H.family != TPE_CAT && (H.flags & (TPE_HAS_LOW | TPE_HAS_HIGH)) != 0;
-#pragma unroll 1
-  for (int k = threadIdx.x; k < K; k += blockDim.x) {
-    double pw = w[k];
-    if (bounded) {
-      const double s2 = 1.4142135623730951 * sg[k];
-      const double za = (H.low - mu[k]) / s2, zb = (H.high - mu[k]) / s2;
-      double b, m;
-      unsigned char md;
-      if (za >= 0.0) {         // upper half: Q(z) = erfc(z) / 2
-        b = 0.5 * erfc(za); m = b - 0.5 * erfc(zb); md = 1;
-      } else if (zb <= 0.0) {  // lower half: Phi(z) = erfc(-z) / 2
-        b = 0.5 * erfc(-za); m = 0.5 * erfc(-zb) - b; md = 2;
-      } else {
-        b = 0.5 * erfc(-za); m = 0.5 * erfc(-zb) - b; md = 0;
-      }
-      m = m > 0.0 ? m : 0.0;
-      T.base[k] = b; T.mass[k] = m; T.mode[k] = md;
-      pw *= m;
-    }
-    T.cdf[k] = pw;
-  }
-  __syncthreads();
-  block_inclusive_scan(T.cdf, K, T.wtot);
-}
-
-__device__ double draw_table(const tpe_hp &H, int K, const double *__restrict__ mu,
-                             const double *__restrict__ sg, const DrawTable &T,
-                             uint64_t seed, uint64_t gi, uint32_t stream) {
-  const Draw d = draw4(seed, gi, stream, 0);
-  const int k = pick_cdf(T.cdf, K, d.u0);
-  if (H.family == TPE_CAT) return (double)k;
-  double x;
-  if (H.flags & (TPE_HAS_LOW | TPE_HAS_HIGH)) {
-    // one tail probability q and side: x = mu + side * sqrt2 sigma erfcinv(2q)
-    const double s2 = 1.4142135623730951 * sg[k], b = T.base[k], m = T.mass[k];
-    const int md = T.mode[k];
-    double q, side;
-    if (md == 1) { q = b - d.u1 * m; side = 1.0; }        // upper tail Q
-    else {
-      const double pp = b + d.u1 * m;                      // Phi
-      if (md == 2 || pp < 0.5) { q = pp; side = -1.0; }
-      else { q = 1.0 - pp; side = 1.0; }
-    }
-    x = mu[k] + side * s2 * erfcinv(2.0 * q);
-    if (!(x >= H.low)) x = H.low;  // rounding at the bounds / zero-mass picks
-    if (!(x < H.high)) x = nextafter(H.high, -INFINITY);
-  } else {
-    x = mu[k] + sg[k] * (sqrt(-2.0 * log(1.0 - d.u1)) * cospi(2.0 * d.u2));
-  }
-  if (H.family == TPE_LGMM) x = exp(x);
-  if (H.flags & TPE_HAS_Q) x = rint(x / H.q) * H.q;
-  return x;
-}
-
-// s is wave-uniform: select the inline seed with an unrolled compare chain
-// (a dynamic index into the by-value argument would copy it to scratch)
-__device__ __forceinline__ uint64_t suggestion_seed(const ScoreArgs &A, int s) {
-  if (s >= A.n_inline_seeds) return A.seeds[s];
-  uint64_t v = A.seed_inline[0];
-#pragma unroll
-  for (int i = 1; i < kInlineSeeds; ++i) v = (s == i) ? A.seed_inline[i] : v;
-  return v;
-}
 
 // Candidate draws of one level (all its hps): grid = (blocks, hps of the
 // level, suggestions), one candidate per thread per step.  Counter = (global
@@ -488,6 +286,11 @@ hipError_t launch_micro(int which, int blocks, int iters, double *sink, hipStrea
 // ------------------------------------------------------------------------
 // launch wrappers
 // ------------------------------------------------------------------------
+bool is_draw_kernel_fn(const void *f) {
+  return f == reinterpret_cast<const void *>(&k_draw<true>) ||
+         f == reinterpret_cast<const void *>(&k_draw<false>);
+}
+
 hipError_t launch_draw(const ScoreArgs &a, bool table, hipStream_t st) {
   if (a.n_slots <= 0 || a.n_suggest <= 0 || a.n_cand <= 0) return hipSuccess;
   const unsigned gx = (unsigned)((a.n_cand + kDrawThreads - 1) / kDrawThreads);

@@ -121,15 +121,17 @@ def suggest(new_ids, domain, trials, seed,
     with st.lock:
         plan = st.plan
         plan.set_history(losses, vals, active)
-        plan.fit(gamma=gamma, prior_weight=prior_weight, lf=DEFAULT_LF)
         if rng_stream == 'philox':
-            res = plan.suggest([int(seed)], int(n_EI_candidates))[0]
+            # fit + sample + score + argmax in one engine call (graph replay)
+            res = plan.fit_suggest([int(seed)], int(n_EI_candidates), gamma=gamma,
+                                   prior_weight=prior_weight, lf=DEFAULT_LF)[0]
             chosen = {}
             for h in cs.hps:
                 r = res[h.index]
                 if r['active'] and r['index'] >= 0:
                     chosen[h.label] = _fmt(h, r['value'])
         elif rng_stream == 'numpy':
+            plan.fit(gamma=gamma, prior_weight=prior_weight, lf=DEFAULT_LF)
             chosen = _suggest_numpy_stream(cs, plan, seed, int(n_EI_candidates))
         else:
             raise ValueError('rng_stream must be "philox" or "numpy"')

@@ -172,6 +172,17 @@ int tpe_plan_suggest(tpe_plan_t p, const uint64_t *seeds, int64_t n_suggest,
                      int64_t n_cand, int64_t cand_begin, int32_t level,
                      tpe_result *out, int32_t out_on_device, void *stream);
 
+/* tpe_plan_fit + tpe_plan_suggest (all levels, cand_begin 0) in one call:
+ * the tpe.suggest posterior evaluation for one history.  Repeated calls of
+ * one shape (prior_weight, lf, n_suggest <= 8, n_candidates, stream) may
+ * replay a captured hipGraph of the whole step, patched with this call's
+ * history length and seeds (opt-in: TPE_GRAPH=1 in the environment; the
+ * default enqueues the step's kernels back to back).                      */
+int tpe_plan_fit_suggest(tpe_plan_t p, double gamma, int32_t gamma_cap,
+                         double prior_weight, int32_t lf, const uint64_t *seeds,
+                         int64_t n_suggest, int64_t n_cand, tpe_result *out,
+                         int32_t out_on_device, void *stream);
+
 /* Results [n_suggest][n_hp] of the last tpe_plan_suggest (copy), and the
  * device address where the plan keeps them (valid until the next call).   */
 int tpe_plan_get_results(tpe_plan_t p, tpe_result *out, int32_t out_on_device,
@@ -191,9 +202,10 @@ int tpe_plan_score_candidates(tpe_plan_t p, int32_t hp, const double *x,
                               int64_t n, double *llik_b, double *llik_a,
                               int64_t *best_index, double *best_score);
 
-/* Device time (ms) of the last tpe_plan_suggest's scoring launches, from
- * HIP events on the plan's stream; and the (candidate, component) pairs
- * they evaluated.                                                          */
+/* Device time (ms) of the last tpe_plan_suggest, from HIP events on the
+ * plan's stream (recorded only while tpe_plan_profile is on, else NaN: an
+ * event record drains the pipeline between launches); and the (candidate,
+ * component) pairs it evaluated.                                           */
 int tpe_plan_last_stats(tpe_plan_t p, double *score_ms, double *pairs);
 
 /* Per-kernel profiling: record HIP events around each of the next `capacity`

@@ -239,3 +239,22 @@ def test_candidate_sharding_invariance_and_device_merge():
     torch.cuda.synchronize()
     np.testing.assert_array_equal(merged['index'], full['index'])
     np.testing.assert_array_equal(merged['value'], full['value'])
+
+
+def test_fit_suggest_graph_replay_matches_eager():
+    """tpe_plan_fit_suggest: the first call of a shape runs eagerly, the
+    second captures a hipGraph, later ones replay it with the history length
+    and seeds patched; every call must equal fit() + suggest() bit for bit,
+    across seeds and a growing history."""
+    meta, d, dom, trials = _fixture_trials('cfg2')
+    tpe.suggest([meta['new_id']], dom, trials, 7, n_EI_candidates=64)
+    plan = dom._tpe_state.plan
+    from hyperopt_amd.tpe import build_history
+    _, losses, vals, active = build_history(dom, trials, dom.space.labels)
+    n = losses.size
+    for i, (m, seed) in enumerate([(n, 3), (n, 4), (n, 5), (n - 7, 6), (n - 7, 3), (n, 9)]):
+        plan.set_history(losses[:m], vals[:, :m], active[:, :m])
+        got = plan.fit_suggest([seed], 512)
+        plan.fit()
+        want = plan.suggest([seed], 512)
+        np.testing.assert_array_equal(got.view(np.uint8), want.view(np.uint8), err_msg=str(i))
