@@ -175,7 +175,31 @@ def main():
         score_ms, launches = ms, n
         if pairs:
             kinds[name] = pairs
+    lat_ms, lat_launches, lat_pairs = plan.profile_read(5)
     plan.profile(0)
+    # A/B: the same steps with every quantized candidate scored on its own
+    # (no value lattice), timed like the main region
+    no_lat = None
+    if lat_launches:
+        plan.set_lattice(False)
+        for i in range(max(1, args.warmup)):
+            step(i)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        t1 = time.perf_counter()
+        for i in range(args.steps):
+            step(args.warmup + i)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        e1 = time.perf_counter() - t1
+        t = torch.tensor([e1], dtype=torch.float64, device='cuda')
+        if dist:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        e1 = float(t.item())
+        no_lat = dict(value=world * pairs_step * args.steps / e1, ms_per_step=1e3 * e1 / args.steps)
+        plan.set_lattice(True)
     # census pass (its counting variant of the kernel is not timed)
     plan.census(True)
     for i in range(n_prof):
@@ -224,6 +248,14 @@ def main():
                 fp64_fma_peak_flops=eng.microbench(1), exp_f32_peak_per_s=eng.microbench(0),
                 erf_f64_peak_per_s=eng.microbench(2))
 
+    if lat_launches:
+        roof['lattice'] = dict(
+            kernel='k_lattice (bounded quantized hps: every lattice value j*q scored once per '
+                   'suggest call, candidates look their lpdfs up in k_score; bit-identical)',
+            avg_launch_ms=lat_ms, launches_per_step=lat_launches / n_prof,
+            pairs_per_launch=lat_pairs,
+            erf_pair_rate_per_s=lat_pairs / (lat_ms * 1e-3) if lat_ms else None,
+            frac_of_erf_pair_peak=(lat_pairs / (lat_ms * 1e-3)) / erf_peak if lat_ms else None)
     cpu = None
     if not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline(dom, losses, vals, active, n_cand if args.config == 'cfg2' else 4096,
@@ -253,6 +285,7 @@ def main():
             'parallelism': 'replicas' if world > 1 else 'single',
         },
         'roofline': roof,
+        'per_candidate_quantized': no_lat,
         'cpu_baseline': cpu,
     }
     print(json.dumps(line))

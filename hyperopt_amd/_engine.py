@@ -39,6 +39,7 @@ EXPORTS = (
     'tpe_plan_suggest', 'tpe_plan_merge', 'tpe_plan_score_candidates', 'tpe_plan_last_stats',
     'tpe_plan_profile', 'tpe_plan_profile_read', 'tpe_microbench', 'tpe_plan_get_results',
     'tpe_plan_results_device', 'tpe_plan_census', 'tpe_plan_fit_suggest',
+    'tpe_plan_set_lattice',
 )
 
 
@@ -141,6 +142,7 @@ def load_library(path: str = LIB_PATH):
             'tpe_plan_get_results': (C.c_int, [vp, vp, i32, vp]),
             'tpe_plan_results_device': (vp, [vp]),
             'tpe_plan_census': (C.c_int, [vp, i32, C.POINTER(i64)]),
+            'tpe_plan_set_lattice': (C.c_int, [vp, i32]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -451,6 +453,13 @@ class Plan(object):
             e.check(e.lib.tpe_plan_profile_read(self.p, int(kind), C.byref(ms), C.byref(n),
                                                 C.byref(pairs)))
         return ms.value, n.value, pairs.value
+
+    def set_lattice(self, enable):
+        """Score bounded quantized hps on their value lattice (default) or
+        every candidate on its own (tpe_plan_set_lattice)."""
+        e = self.engine
+        with e.lock:
+            e.check(e.lib.tpe_plan_set_lattice(self.p, int(bool(enable))))
 
     def census(self, enable):
         """Quantized-pair census since the last call (total, live, evaluated);

@@ -62,6 +62,11 @@ struct tpe_plan {
   uint32_t *d_ticket = nullptr;
   std::vector<uint64_t> h_seeds;  // this call's seeds (inline kernel args when <= 8)
   bool has_erf = false;
+  // value lattices of the bounded quantized hps (KIND_LAT, k_lattice)
+  std::vector<LatInfo> lat;
+  LatInfo *d_lat_info = nullptr;
+  double2 *d_lat = nullptr;
+  bool lattice_on = true;
   hipEvent_t ev_fork = nullptr, ev_join[8] = {};
   double *d_ext = nullptr, *d_lb = nullptr, *d_la = nullptr;
   size_t ext_cap = 0;
@@ -153,7 +158,7 @@ void plan_free_buffers(tpe_plan *p) {
                   p->d_losses, p->d_vals, p->d_active, p->d_below, p->d_mw, p->d_mmu,
                   p->d_msig, p->d_scratch, p->d_info, p->d_coef, p->d_results, p->d_seeds,
                   p->d_partial, p->d_ext, p->d_lb, p->d_la, p->d_cand, p->d_cpos,
-                  p->d_ticket, p->d_sortbuf, p->d_census};
+                  p->d_ticket, p->d_sortbuf, p->d_census, p->d_lat_info, p->d_lat};
   for (void *b : bufs) dfree(b);
   if (p->ev0) (void)hipEventDestroy(p->ev0);
   if (p->ev1) (void)hipEventDestroy(p->ev1);
@@ -198,6 +203,28 @@ int validate_space(tpe_engine *h, const tpe_space *sp) {
 }
 
 // level(h) = 0 without conditions, else 1 + max(level(parent))
+// The value lattice of a bounded quantized hp (LatInfo): drawn values lie in
+// [low, high) (GMM) or [exp(low), exp(high)] (LGMM) before rounding to j * q;
+// two indices of margin on each side absorb host/device exp and division
+// rounding.  R = 0 (no lattice) for unbounded or huge ranges.
+LatInfo lattice_of(const tpe_hp &x) {
+  LatInfo L{0, 0, 0, 0};
+  const int k = score_kind(x);
+  if (k != KIND_ERF_G && k != KIND_ERF_L) return L;
+  if (!(x.flags & TPE_HAS_LOW) || !(x.flags & TPE_HAS_HIGH) || !(x.q > 0.0)) return L;
+  double lo = x.low, hi = x.high;
+  if (k == KIND_ERF_L) {
+    lo = std::exp(lo);
+    hi = std::exp(hi);
+  }
+  const double a = std::rint(lo / x.q) - 2.0, b = std::rint(hi / x.q) + 2.0;
+  if (!(std::fabs(a) < 1e15 && std::fabs(b) < 1e15) || b - a + 1.0 > (double)kLatMaxR)
+    return L;
+  L.j0 = (int64_t)a;
+  L.R = (int32_t)(b - a + 1.0);
+  return L;
+}
+
 int compute_levels(tpe_engine *h, tpe_plan *p) {
   std::vector<int> lev(p->P, -1);
   for (int iter = 0; iter <= p->P; ++iter) {
@@ -221,9 +248,15 @@ int compute_levels(tpe_engine *h, tpe_plan *p) {
     nl = std::max(nl, lev[i] + 1);
   }
   p->levels.assign(nl, {});
-  // heaviest lpdf kind first: the scoring grid's low slots are dispatched
-  // first, so the long quantized tiles do not form the launch's tail
-  for (int kind : {KIND_ERF_L, KIND_ERF_G, KIND_LSE_L, KIND_LSE_G, KIND_CAT})
+  // quantized hps with a value lattice first (run_level scores them on it),
+  // then the heaviest lpdf kind first: the scoring grid's low slots are
+  // dispatched first, so the long quantized tiles do not form the launch's tail
+  for (int lat : {1, 0})
+    for (int kind : {KIND_ERF_L, KIND_ERF_G})
+      for (int i = 0; i < p->P; ++i)
+        if (score_kind(p->hps[i]) == kind && (lattice_of(p->hps[i]).R > 0) == (lat == 1))
+          p->levels[lev[i]].push_back(i);
+  for (int kind : {KIND_LSE_L, KIND_LSE_G, KIND_CAT})
     for (int i = 0; i < p->P; ++i)
       if (score_kind(p->hps[i]) == kind) p->levels[lev[i]].push_back(i);
   p->level_off.assign(nl + 1, 0);
@@ -268,7 +301,16 @@ int plan_build(tpe_engine *h, const tpe_space *sp, int64_t max_trials, tpe_plan 
     if (k == KIND_ERF_G || k == KIND_ERF_L) p->has_erf = true;
   }
   const int64_t slots = 2 * (int64_t)p->P;
+  p->lat.assign(p->P, LatInfo{0, 0, 0, 0});
+  int64_t lat_total = 0;
+  for (int i = 0; i < p->P; ++i) {
+    p->lat[i] = lattice_of(p->hps[i]);
+    p->lat[i].off = lat_total;
+    lat_total += p->lat[i].R;
+  }
   CKH(hipSetDevice(h->device));
+  CKH(dalloc(&p->d_lat_info, p->P));
+  CKH(dalloc(&p->d_lat, std::max<int64_t>(1, lat_total)));
   CKH(dalloc(&p->d_hps, p->P));
   CKH(dalloc(&p->d_cp, p->cond_parent.size()));
   CKH(dalloc(&p->d_cb, p->cond_branch.size()));
@@ -299,6 +341,8 @@ int plan_build(tpe_engine *h, const tpe_space *sp, int64_t max_trials, tpe_plan 
   for (int i = 0; i < p->P; ++i) all[i] = i;
   hipStream_t st = h->stream;
   CKH(hipMemcpyAsync(p->d_hps, p->hps.data(), p->P * sizeof(tpe_hp), hipMemcpyHostToDevice, st));
+  CKH(hipMemcpyAsync(p->d_lat_info, p->lat.data(), p->P * sizeof(LatInfo), hipMemcpyHostToDevice,
+                     st));
   if (!p->cond_parent.empty()) {
     CKH(hipMemcpyAsync(p->d_cp, p->cond_parent.data(), p->cond_parent.size() * 4, hipMemcpyHostToDevice, st));
     CKH(hipMemcpyAsync(p->d_cb, p->cond_branch.data(), p->cond_branch.size() * 4, hipMemcpyHostToDevice, st));
@@ -423,6 +467,8 @@ ScoreArgs base_args(tpe_plan *p, int64_t n_sug) {
   a.kcap = p->kcap;
   a.n_hp = p->P;
   a.n_suggest = (int32_t)n_sug;
+  a.lat_info = p->d_lat_info;
+  a.lat = p->d_lat;
   return a;
 }
 
@@ -485,6 +531,35 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
     if (k == KIND_CAT) kmax = std::max<int64_t>(kmax, p->hps[hp].upper);
   }
   const bool table_draw = kmax <= kTabCap;
+  // the level's leading quantized hps with a value lattice are scored on it
+  // (k_lattice once per call, then lookups) when no lattice is larger than
+  // the candidate count; the other quantized hps per candidate (bucketed)
+  int32_t n_lat = 0;
+  int64_t rmax = 0;
+  while (n_lat < n_level && (kinds[n_lat] == KIND_ERF_G || kinds[n_lat] == KIND_ERF_L) &&
+         p->lat[p->levels[level][n_lat]].R > 0) {
+    rmax = std::max<int64_t>(rmax, p->lat[p->levels[level][n_lat]].R);
+    ++n_lat;
+  }
+  const bool lat_level = n_lat > 0 && p->lattice_on && rmax <= n_cand * n_sug &&
+                         2 * ((p->kcap + 15) / 16) <= (int64_t)kLatChunks;
+  if (!lat_level) n_lat = 0;
+  if (lat_level) {
+    for (int i = 0; i < n_lat; ++i) kinds[i] = KIND_LAT;
+    erf_level = false;  // per-candidate quantized slots left after the lattice ones?
+    for (int i = n_lat; i < n_level; ++i)
+      erf_level |= kinds[i] == KIND_ERF_G || kinds[i] == KIND_ERF_L;
+    ScoreArgs la = base_args(p, n_sug);
+    tpe_plan::Prof *pr = nullptr;
+    if (p->prof_cap > 0 && p->prof[1].n < p->prof_cap) pr = &p->prof[1];
+    if (pr) CKH(hipEventRecord(pr->a[pr->n], st));
+    CKH(launch_lattice(la, lvl, n_lat, rmax, p->d_lat, st));
+    if (pr) {
+      CKH(hipEventRecord(pr->b[pr->n], st));
+      pr->pairs[pr->n] = (double)level;
+      pr->n++;
+    }
+  }
   const int64_t budget = (int64_t)64 << 20;  // doubles
   const int64_t chunk = std::max<int64_t>(
       1, std::min<int64_t>(std::max<int64_t>(n_cand, 1),
@@ -514,7 +589,7 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
     for (int i = 0; i < kInlineSeeds && i < n_sug; ++i) a.seed_inline[i] = p->h_seeds[i];
     a.n_inline_seeds = (int32_t)std::min<int64_t>(n_sug, kInlineSeeds);
     CKH(launch_draw(a, table_draw, st));
-    if (erf_level) CKH(launch_bucket(a, p->d_cpos, st));
+    if (erf_level) CKH(launch_bucket(a, n_lat, p->d_cpos, st));
     a.cand_pos = erf_level ? p->d_cpos : nullptr;
     rc = score_launch(h, p, a, erf_level, cn, st, true);
     if (rc) return rc;
@@ -1180,10 +1255,30 @@ int tpe_plan_profile(tpe_plan_t p, int32_t capacity) {
 
 int tpe_plan_profile_read(tpe_plan_t p, int32_t kind, double *avg_ms, int64_t *launches,
                           double *pairs_per_launch) {
-  if (!p || kind < 0 || kind > KIND_CAT) return TPE_E_INVALID;
+  if (!p || kind < 0 || kind > KIND_LAT) return TPE_E_INVALID;
   tpe_engine *h = p->eng;
   CKH(hipSetDevice(h->device));
   CKH(hipDeviceSynchronize());
+  if (kind == KIND_LAT) {  // k_lattice launches: lattice points x (K_b + K_a)
+    auto &pl = p->prof[1];
+    std::vector<MixInfo> info(2 * (size_t)p->P);
+    CKH(hipMemcpy(info.data(), p->d_info, info.size() * sizeof(MixInfo), hipMemcpyDeviceToHost));
+    double tot = 0.0, pairs = 0.0;
+    for (int64_t i = 0; i < pl.n; ++i) {
+      float ms = 0.f;
+      CKH(hipEventElapsedTime(&ms, pl.a[i], pl.b[i]));
+      tot += ms;
+      for (int hp : p->levels[(int)pl.pairs[i]]) {
+        const int k = score_kind(p->hps[hp]);
+        if (k == KIND_ERF_G || k == KIND_ERF_L)
+          pairs += (double)p->lat[hp].R * ((double)info[2 * hp].K + info[2 * hp + 1].K);
+      }
+    }
+    if (avg_ms) *avg_ms = pl.n ? tot / pl.n : 0.0;
+    if (launches) *launches = pl.n;
+    if (pairs_per_launch) *pairs_per_launch = pl.n ? pairs / pl.n : 0.0;
+    return TPE_OK;
+  }
   auto &pr = p->prof[0];  // every scoring launch (all lpdf kinds of a level)
   double tot = 0.0, pairs = 0.0;
   // this kind's pairs in those launches: components per candidate of the
@@ -1212,6 +1307,13 @@ int tpe_plan_profile_read(tpe_plan_t p, int32_t kind, double *avg_ms, int64_t *l
   if (launches) *launches = pr.n;
   if (pairs_per_launch) *pairs_per_launch = pr.n ? pairs / pr.n : 0.0;
   return TPE_OK;  // the ring is re-armed by tpe_plan_profile
+}
+
+int tpe_plan_set_lattice(tpe_plan_t p, int32_t enable) {
+  if (!p) return TPE_E_INVALID;
+  if (p->lattice_on != (enable != 0)) graph_reset(p);
+  p->lattice_on = enable != 0;
+  return TPE_OK;
 }
 
 int tpe_plan_census(tpe_plan_t p, int32_t enable, int64_t *counts) {

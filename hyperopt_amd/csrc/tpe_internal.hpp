@@ -15,7 +15,10 @@ constexpr int kMaxLeaves = 160;  // numpy pairwise leaves per 8192 chunk (<=128)
 
 // Per (hp, side) mixture slot, written by k_fit / k_prep.
 // scoring kernel instantiations (lpdf kinds)
-enum { KIND_LSE_G = 0, KIND_LSE_L = 1, KIND_ERF_G = 2, KIND_ERF_L = 3, KIND_CAT = 4 };
+// KIND_LAT: a quantized hp scored on its value lattice (k_lattice) -- the
+// scoring launch only looks its candidates up (run_level picks it per level)
+enum { KIND_LSE_G = 0, KIND_LSE_L = 1, KIND_ERF_G = 2, KIND_ERF_L = 3, KIND_CAT = 4,
+       KIND_LAT = 5 };
 
 __host__ __device__ inline int score_kind(const tpe_hp &h) {
   if (h.family == TPE_CAT) return KIND_CAT;
@@ -26,9 +29,10 @@ __host__ __device__ inline int score_kind(const tpe_hp &h) {
 
 // candidate rows (per lane) of a scoring tile of the kind: 64 * rows candidates
 __host__ __device__ constexpr int tile_rows(int kind) {
-  return (kind == KIND_ERF_G || kind == KIND_ERF_L) ? 1 : kind == KIND_CAT ? 4 : 2;
+  return (kind == KIND_ERF_G || kind == KIND_ERF_L) ? 1
+         : (kind == KIND_CAT || kind == KIND_LAT) ? 4 : 2;
 }
-constexpr int kMaxGroups = 5;  // lpdf kinds: at most one group of each per launch
+constexpr int kMaxGroups = 8;  // runs of one lpdf kind per launch (a level has <= 7)
 
 struct MixInfo {
   int32_t K;        // components (categorical: upper)
@@ -73,6 +77,21 @@ static_assert(sizeof(Partial) == sizeof(tpe_result), "layout");
 
 constexpr int kInlineSeeds = 8;  // suggestion seeds passed by value
 
+// Value lattice of a bounded quantized hp: every drawn candidate is j * q for
+// an integer j in [j0, j0 + R) (GMM: low <= x < high before rounding, LGMM:
+// exp of such a draw; one index of margin on each side).  Its lpdf pair is
+// kept at lat[off + j - j0] (k_lattice).  R = 0: no lattice.
+struct LatInfo {
+  int64_t j0;
+  int64_t off;
+  int32_t R;
+  int32_t pad;
+};
+// k_lattice keeps one partial sum per 16-component chunk of both mixtures
+// of a point in LDS: mixtures of up to 16 * kLatChunks / 2 components
+constexpr int kLatChunks = 8192;
+constexpr int64_t kLatMaxR = (int64_t)1 << 22;  // lattice points per hp
+
 struct ScoreArgs {
   uint64_t seed_inline[kInlineSeeds];
   int32_t n_inline_seeds;
@@ -108,6 +127,8 @@ struct ScoreArgs {
   int32_t force_active;      // ignore conditions (operator-level scoring)
   int32_t accumulate;        // merge with results of an earlier candidate chunk
   unsigned long long *census;  // optional [3]: quantized pairs total / live / executed
+  const LatInfo *lat_info;   // [P] value lattices (KIND_LAT slots)
+  const double2 *lat;        // lattice (lpdf below, lpdf above) pairs
 };
 
 // Arguments of the fit kernels (tpe_fit.hip), one block per (hp, side) slot.
@@ -141,9 +162,15 @@ hipError_t launch_prep(const tpe_hp *hps, int32_t n_hp, const double *mw,
                        Coef *coef, int64_t kcap, double *scratch,
                        hipStream_t st);
 hipError_t launch_score(const ScoreArgs &a, bool has_erf, hipStream_t st);
+// lpdf pairs of every lattice point of the n_lat hps lat_hps[] (one block of
+// kLatThreads per point; rmax = largest R), written to lat_out
+constexpr int kLatThreads = 1024;
+hipError_t launch_lattice(const ScoreArgs &a, const int32_t *lat_hps, int32_t n_lat, int64_t rmax,
+                          double2 *lat_out, hipStream_t st);
 constexpr int kTabCap = 2048;  // below-mixture components of the LDS draw table
 hipError_t launch_draw(const ScoreArgs &a, bool table, hipStream_t st);
-hipError_t launch_bucket(const ScoreArgs &a, int32_t *pos_out, hipStream_t st);
+// slots slot_begin .. n_slots-1 (the lattice slots before them are not bucketed)
+hipError_t launch_bucket(const ScoreArgs &a, int32_t slot_begin, int32_t *pos_out, hipStream_t st);
 hipError_t launch_merge(const int32_t *level_hps, int32_t n_slots,
                         int32_t n_suggest, int32_t n_hp, int32_t world,
                         const Partial *gathered, Partial *results,

@@ -63,11 +63,12 @@ __global__ __launch_bounds__(kDrawThreads) void k_draw(ScoreArgs A) {
 // whole wave.  Order inside a bucket is irrelevant: every candidate is
 // scored on its own and the argmax tie-break uses the original index.
 constexpr int kBuckets = 256;
-__global__ __launch_bounds__(1024) void k_bucket(ScoreArgs A, int32_t *__restrict__ pos_out) {
+__global__ __launch_bounds__(1024) void k_bucket(ScoreArgs A, int32_t slot_begin,
+                                                 int32_t *__restrict__ pos_out) {
   extern __shared__ __attribute__((aligned(16))) double dyn_lds[];
   __shared__ int hist[kBuckets];
   __shared__ double red_lo[16], red_hi[16];
-  const int slot = blockIdx.y, s = blockIdx.z;
+  const int slot = slot_begin + (int)blockIdx.y, s = blockIdx.z;
   const int hp = A.level_hps[slot];
   const tpe_hp H = A.hps[hp];
   const int kind = score_kind(H);
@@ -299,10 +300,11 @@ hipError_t launch_draw(const ScoreArgs &a, bool table, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_bucket(const ScoreArgs &a, int32_t *pos_out, hipStream_t st) {
-  if (a.n_slots <= 0 || a.n_suggest <= 0 || a.n_cand <= 0) return hipSuccess;
+hipError_t launch_bucket(const ScoreArgs &a, int32_t slot_begin, int32_t *pos_out, hipStream_t st) {
+  if (a.n_slots <= slot_begin || a.n_suggest <= 0 || a.n_cand <= 0) return hipSuccess;
   const unsigned gx = (unsigned)((a.n_cand + kSortMax - 1) / kSortMax);
-  k_bucket<<<dim3(gx, a.n_slots, a.n_suggest), 1024, (size_t)kSortMax * 9, st>>>(a, pos_out);
+  k_bucket<<<dim3(gx, a.n_slots - slot_begin, a.n_suggest), 1024, (size_t)kSortMax * 9, st>>>(
+      a, slot_begin, pos_out);
   return hipGetLastError();
 }
 

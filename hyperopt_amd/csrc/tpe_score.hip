@@ -164,14 +164,57 @@ struct Census {
   uint32_t total, live, exec;
 };
 
+// Candidate-side bounds of the quantized lpdf, tpe.py:146-152 (GMM) and
+// 284-293 (LGMM: on log scale, lb clipped at 0, both floored at EPS).
+template <bool LOGN>
+__device__ __forceinline__ void quant_bounds(const tpe_hp &H, double x, double &ub, double &lb) {
+  const double hq = H.q / 2.0;
+  if constexpr (!LOGN) {
+    ub = (H.flags & TPE_HAS_HIGH) ? np_minimum(x + hq, H.high) : x + hq;
+    lb = (H.flags & TPE_HAS_LOW) ? np_maximum(x - hq, H.low) : x - hq;
+  } else {
+    const double u = (H.flags & TPE_HAS_HIGH) ? np_minimum(x + hq, exp(H.high)) : x + hq;
+    double l = (H.flags & TPE_HAS_LOW) ? np_maximum(x - hq, exp(H.low)) : x - hq;
+    l = np_maximum(0.0, l);
+    ub = u < 0.0 ? NAN : log(np_maximum(u, kEPS));
+    lb = log(np_maximum(l, kEPS));
+  }
+}
+
+// one quantized term w (Phi(ub) - Phi(lb)) in the reference's operation
+// order (GMM: 0.5 * (1 + erf), LGMM: .5 + .5 * erf; two-stage difference)
+template <bool LOGN>
+__device__ __forceinline__ double erf_term(double zu, double zl, double w) {
+#pragma clang fp contract(off)
+  double cu, cl;
+  if (LOGN) {
+    cu = .5 + .5 * erf(zu);
+    cl = .5 + .5 * erf(zl);
+  } else {
+    cu = 0.5 * (1.0 + erf(zu));
+    cl = 0.5 * (1.0 + erf(zl));
+  }
+  double inc = w * cu;
+  inc -= w * cl;
+  return inc;
+}
+
+// a term whose two erf arguments are beyond 6.5 on one side is an exact 0
+// (erf saturates to +-1 from 5.93)
+__device__ __forceinline__ bool erf_dead(double zu, double zl) {
+  return (zu >= 6.5 && zl >= 6.5) || (zu <= -6.5 && zl <= -6.5);
+}
+
 // the same chunks, quantized: sum_k w (Phi(ub) - Phi(lb)),
 // tpe.py:146-160 (GMM: 0.5 * (1 + erf)) / 284-299 (LGMM: .5 + .5 * erf).
+// Canonical order (k_lattice reproduces it): each chunk is summed in
+// component order from 0, the chunk sums are added to the wave's total.
 // A chunk is skipped when every candidate of the wave is provably beyond
 // 6.6 sigma-units of every one of its components on one side (Coef.w holds
-// 6.6 * max(sqrt(2) sigma, EPS)): all its terms are then exact zeros (erf
-// saturates to +-1 from 5.93).  wlo / whi: the wave's min lb / max ub;
-// `exact` false (a NaN bound) disables the chunk test.  Inside a chunk, a
-// component is skipped when all its terms in the wave are exact zeros.
+// 6.6 * max(sqrt(2) sigma, EPS)): all its terms are then exact zeros.
+// wlo / whi: the wave's min lb / max ub; `exact` false (a NaN bound)
+// disables the chunk test.  Inside a chunk, a component is skipped when all
+// its terms in the wave are exact zeros.
 template <int KR, bool LOGN, bool CENSUS>
 __device__ __forceinline__ void erf_chunks(KDbl *__restrict__ cs, int c0, int nb,
                                            const double (&ub)[KR], const double (&lb)[KR],
@@ -205,44 +248,36 @@ __device__ __forceinline__ void erf_chunks(KDbl *__restrict__ cs, int c0, int nb
         continue;
       }
     }
-  for (int k = k0; k < k1; ++k) {
-    const double cx = cs[coef_off(k, 0)], cy = cs[coef_off(k, 1)];
-    double zu[KR], zl[KR];
-    bool dead_all = true;
+    double pc[KR];
 #pragma unroll
-    for (int r = 0; r < KR; ++r) {
-      zu[r] = (ub[r] - cx) * cy;
-      zl[r] = (lb[r] - cx) * cy;
-      const bool dead = !valid[r] || (zu[r] >= 6.5 && zl[r] >= 6.5) ||
-                        (zu[r] <= -6.5 && zl[r] <= -6.5);
-      dead_all &= dead;
+    for (int r = 0; r < KR; ++r) pc[r] = 0.0;
+    for (int k = k0; k < k1; ++k) {
+      const double cx = cs[coef_off(k, 0)], cy = cs[coef_off(k, 1)];
+      double zu[KR], zl[KR];
+      bool dead_all = true;
+#pragma unroll
+      for (int r = 0; r < KR; ++r) {
+        zu[r] = (ub[r] - cx) * cy;
+        zl[r] = (lb[r] - cx) * cy;
+        const bool dead = !valid[r] || erf_dead(zu[r], zl[r]);
+        dead_all &= dead;
+        if constexpr (CENSUS) {
+          cen.total += valid[r] ? 1u : 0u;
+          cen.live += dead ? 0u : 1u;
+        }
+      }
+      const bool skip = __all(dead_all);
       if constexpr (CENSUS) {
-        cen.total += valid[r] ? 1u : 0u;
-        cen.live += dead ? 0u : 1u;
-      }
-    }
-    const bool skip = __all(dead_all);
-    if constexpr (CENSUS) {
 #pragma unroll
-      for (int r = 0; r < KR; ++r) cen.exec += (valid[r] && !skip) ? 1u : 0u;
-    }
-    if (skip) continue;  // exact zeros for every candidate of the wave
-    const double w = cs[coef_off(k, 2)];
-#pragma unroll
-    for (int r = 0; r < KR; ++r) {
-      double cu, cl;
-      if (LOGN) {
-        cu = .5 + .5 * erf(zu[r]);
-        cl = .5 + .5 * erf(zl[r]);
-      } else {
-        cu = 0.5 * (1.0 + erf(zu[r]));
-        cl = 0.5 * (1.0 + erf(zl[r]));
+        for (int r = 0; r < KR; ++r) cen.exec += (valid[r] && !skip) ? 1u : 0u;
       }
-      double inc = w * cu;
-      inc -= w * cl;
-      prob[r] += inc;
+      if (skip) continue;  // exact zeros for every candidate of the wave
+      const double w = cs[coef_off(k, 2)];
+#pragma unroll
+      for (int r = 0; r < KR; ++r) pc[r] += erf_term<LOGN>(zu[r], zl[r], w);
     }
-  }
+#pragma unroll
+    for (int r = 0; r < KR; ++r) prob[r] += pc[r];
   }
 }
 
@@ -279,7 +314,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
   constexpr int KR = tile_rows(KIND);
   constexpr bool LSE = KIND == KIND_LSE_G || KIND == KIND_LSE_L;
   constexpr bool ERF = KIND == KIND_ERF_G || KIND == KIND_ERF_L;
-  constexpr bool CAT = KIND == KIND_CAT;
+  constexpr bool LAT = KIND == KIND_LAT;  // quantized, looked up on its value lattice
   constexpr bool LOGN = KIND == KIND_LSE_L || KIND == KIND_ERF_L;
   const int s = blockIdx.y;
   const int hp = A.level_hps[slot];
@@ -315,22 +350,11 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
     if constexpr (LSE) {
       y[r] = (LOGN ? log(x[r]) : x[r]) - H.prior_mu;
     } else if constexpr (ERF) {
-      const double hq = H.q / 2.0;
-      if constexpr (!LOGN) {
-        ub[r] = (H.flags & TPE_HAS_HIGH) ? np_minimum(x[r] + hq, H.high) : x[r] + hq;
-        lb[r] = (H.flags & TPE_HAS_LOW) ? np_maximum(x[r] - hq, H.low) : x[r] - hq;
-      } else {
-        const double u =
-            (H.flags & TPE_HAS_HIGH) ? np_minimum(x[r] + hq, exp(H.high)) : x[r] + hq;
-        double l = (H.flags & TPE_HAS_LOW) ? np_maximum(x[r] - hq, exp(H.low)) : x[r] - hq;
-        l = np_maximum(0.0, l);
-        ub[r] = u < 0.0 ? NAN : log(np_maximum(u, kEPS));
-        lb[r] = log(np_maximum(l, kEPS));
-      }
+      quant_bounds<LOGN>(H, x[r], ub[r], lb[r]);
     }
   }
 
-  if constexpr (!CAT) {
+  if constexpr (LSE || ERF) {
     // warm this XCD's L2 with both mixtures' coefficient lines: one dword per
     // 128-B line, issued before the component loop, so the loop's scalar loads
     // hit L2 instead of each group paying a far (MALL / HBM) round trip
@@ -437,6 +461,14 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
     } else if constexpr (ERF) {
       lpb = log(sm.merged[0][r][lane].x) - ib.log_pacc;
       lpa = log(sm.merged[1][r][lane].x) - ia.log_pacc;
+    } else if constexpr (LAT) {
+      const LatInfo L = A.lat_info[hp];
+      const double J = rint(x[r] / H.q);  // x == J * q for every drawn candidate
+      const int64_t idx = fabs(J) < 4.0e15 ? (int64_t)J - L.j0 : -1;
+      const bool in = idx >= 0 && idx < (int64_t)L.R;
+      const double2 v = in ? A.lat[L.off + idx] : make_double2(NAN, NAN);
+      lpb = v.x;
+      lpa = v.y;
     } else {
       const int64_t c = (int64_t)x[r];
       const bool in = (x[r] >= 0.0) && (c < ib.K) && ((double)c == x[r]);
@@ -513,8 +545,91 @@ void k_score(ScoreArgs A) {
     case KIND_LSE_L: score_tile<KIND_LSE_L, CENSUS>(A, sm, slot, tile, nt); break;
     case KIND_ERF_G: if constexpr (ERFK) score_tile<KIND_ERF_G, CENSUS>(A, sm, slot, tile, nt); break;
     case KIND_ERF_L: if constexpr (ERFK) score_tile<KIND_ERF_L, CENSUS>(A, sm, slot, tile, nt); break;
+    case KIND_LAT: score_tile<KIND_LAT, CENSUS>(A, sm, slot, tile, nt); break;
     default: score_tile<KIND_CAT, CENSUS>(A, sm, slot, tile, nt); break;
   }
+}
+
+// Value-lattice scoring of the bounded quantized hps (KIND_LAT).  A drawn
+// candidate of such an hp is one of R lattice values j * q, and its lpdf
+// depends on that value only, so both lpdfs are evaluated once per lattice
+// point and shared by every candidate and every suggestion of the call.
+// One block per (point, hp): lane t takes component 16 * c + (t & 15) of
+// chunk c = t / 16 of the below mixture, then of the above mixture; a chunk is
+// summed in component order by its 16 lanes, and thread 0 / 1 adds the chunk
+// sums of the below / above mixture in erf_chunks' canonical order (chunk c
+// to the total of "wave" c mod kWaves, totals in wave order), so a lattice
+// lpdf is bit-identical to the per-candidate kernel's for that value.
+template <bool LOGN>
+__device__ __forceinline__ void lattice_point(const ScoreArgs &A, const tpe_hp &H, int hp,
+                                              const LatInfo &L, int64_t pt, double *csum,
+                                              double2 *__restrict__ out) {
+#pragma clang fp contract(off)
+  const double x = (double)(L.j0 + pt) * H.q;
+  double ub, lb;
+  quant_bounds<LOGN>(H, x, ub, lb);
+  const int64_t sb = 2 * (int64_t)hp;
+  const MixInfo ib = A.info[sb], ia = A.info[sb + 1];
+  const int ncb = (ib.K + kChunk - 1) / kChunk, nca = (ia.K + kChunk - 1) / kChunk;
+  const int nch = ncb + nca;
+  const double *cb = reinterpret_cast<const double *>(A.coef + sb * A.kcap);
+  const double *ca = reinterpret_cast<const double *>(A.coef + (sb + 1) * A.kcap);
+  const int seg = (threadIdx.x & 63) & ~(kChunk - 1), j = threadIdx.x & (kChunk - 1);
+  for (int t0 = 0; t0 < kChunk * nch; t0 += blockDim.x) {
+    const int c = (t0 + (int)threadIdx.x) / kChunk;
+    double inc = 0.0;
+    if (c < nch) {
+      const bool above = c >= ncb;
+      const int k = (above ? c - ncb : c) * kChunk + j;
+      if (k < (above ? ia.K : ib.K)) {
+        const double *cs = above ? ca : cb;
+        const double cx = cs[coef_off(k, 0)], cy = cs[coef_off(k, 1)];
+        const double zu = (ub - cx) * cy, zl = (lb - cx) * cy;
+        if (!erf_dead(zu, zl)) inc = erf_term<LOGN>(zu, zl, cs[coef_off(k, 2)]);
+      }
+    }
+    double pc = 0.0;  // the chunk in component order
+#pragma unroll
+    for (int i = 0; i < kChunk; ++i) pc += __shfl(inc, seg + i, 64);
+    if (j == 0 && c < nch) csum[c] = pc;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    const int above = threadIdx.x;
+    const int c0 = above ? ncb : 0, n = above ? nca : ncb;
+    double tot = 0.0;
+    for (int w = 0; w < kWaves; ++w) {
+      double sw = 0.0;
+      for (int c = w; c < n; c += kWaves) sw += csum[c0 + c];
+      tot = w == 0 ? sw : tot + sw;
+    }
+    const double lp = log(tot) - (above ? ia.log_pacc : ib.log_pacc);
+    double *o = reinterpret_cast<double *>(out + L.off + pt);
+    o[above] = lp;
+  }
+}
+
+__global__ __launch_bounds__(kLatThreads) void k_lattice(ScoreArgs A,
+                                                          const int32_t *__restrict__ lat_hps,
+                                                          double2 *__restrict__ out) {
+  extern __shared__ double csum[];  // [chunks of both mixtures]
+  const int hp = lat_hps[blockIdx.y];
+  const LatInfo L = A.lat_info[hp];
+  const int64_t pt = blockIdx.x;
+  if (pt >= L.R) return;
+  const tpe_hp H = A.hps[hp];
+  if (H.family == TPE_LGMM) lattice_point<true>(A, H, hp, L, pt, csum, out);
+  else lattice_point<false>(A, H, hp, L, pt, csum, out);
+}
+
+hipError_t launch_lattice(const ScoreArgs &a, const int32_t *lat_hps, int32_t n_lat, int64_t rmax,
+                          double2 *lat_out, hipStream_t st) {
+  if (n_lat <= 0 || rmax <= 0) return hipSuccess;
+  const int64_t nch = 2 * ((a.kcap + kChunk - 1) / kChunk);
+  if (nch > kLatChunks || rmax > kLatMaxR) return hipErrorInvalidValue;
+  k_lattice<<<dim3((unsigned)rmax, (unsigned)n_lat), kLatThreads, (size_t)nch * sizeof(double),
+              st>>>(a, lat_hps, lat_out);
+  return hipGetLastError();
 }
 
 hipError_t launch_score(const ScoreArgs &a, bool has_erf, hipStream_t st) {

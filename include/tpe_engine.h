@@ -212,11 +212,21 @@ int tpe_plan_last_stats(tpe_plan_t p, double *score_ms, double *pairs);
  * scoring launches (one per level and candidate chunk; every lpdf kind of the
  * level), then read their average device duration and, for one lpdf kind
  * (0 LSE-GMM, 1 LSE-LGMM, 2 ERF-GMM, 3 ERF-LGMM, 4 categorical), the
- * (candidate, component) pairs per launch of that kind's active hps.
+ * (candidate, component) pairs per launch of that kind's active hps; kind 5
+ * reads the value-lattice launches instead (their average duration and
+ * lattice points x components per launch).
  * tpe_plan_profile also clears the ring (capacity 0: off).                  */
 int tpe_plan_profile(tpe_plan_t p, int32_t capacity);
 int tpe_plan_profile_read(tpe_plan_t p, int32_t kind, double *avg_ms,
                           int64_t *launches, double *pairs_per_launch);
+
+/* Bounded quantized hps (quniform / qloguniform with finite bounds) are by
+ * default scored on their value lattice: each distinct value j * q a drawn
+ * candidate can take is scored once per suggest call and looked up by every
+ * candidate (bit-identical lpdfs; chosen when the lattice is no larger than
+ * the candidate count).  enable = 0 scores every candidate on its own (the
+ * tpe.py:146-160 / 284-299 work as written), for A/B measurement and tests. */
+int tpe_plan_set_lattice(tpe_plan_t p, int32_t enable);
 
 /* Roofline accounting: read (counts may be NULL) and clear the census of the
  * quantized-kind scoring work since the last call -- counts[0] valid

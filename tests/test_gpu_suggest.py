@@ -258,3 +258,28 @@ def test_fit_suggest_graph_replay_matches_eager():
         plan.fit()
         want = plan.suggest([seed], 512)
         np.testing.assert_array_equal(got.view(np.uint8), want.view(np.uint8), err_msg=str(i))
+
+
+@pytest.mark.parametrize('name', ['cfg2', 'many_dists', 'cond', 'cfg3_small'])
+def test_value_lattice_bitwise_equals_per_candidate(name):
+    """Bounded quantized hps scored once per lattice value (k_lattice, the
+    default) give the same scores, values and indices, bit for bit, as
+    scoring every candidate on its own -- for single and batched suggestions
+    and several candidate counts; the lattice launch must actually run."""
+    meta, d, dom, trials = _fixture_trials(name)
+    tpe.suggest([meta['new_id']], dom, trials, 7, n_EI_candidates=64)
+    plan = dom._tpe_state.plan
+    ran = 0
+    for seeds, n in [([3], 4096), ([4, 5, 6], 2048), ([8], 20000), ([9], 300)]:
+        plan.set_lattice(True)
+        plan.profile(16)
+        got = plan.suggest(seeds, n)
+        ran += plan.profile_read(5)[1]
+        plan.profile(0)
+        plan.set_lattice(False)
+        want = plan.suggest(seeds, n)
+        np.testing.assert_array_equal(got.view(np.uint8), want.view(np.uint8),
+                                      err_msg='%s %s %d' % (name, seeds, n))
+    plan.set_lattice(True)
+    has_q = any(h.dist in ('quniform', 'qloguniform') for h in dom.space.hps)
+    assert (ran > 0) == has_q, (ran, has_q)
