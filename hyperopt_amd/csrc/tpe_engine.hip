@@ -16,6 +16,10 @@
 
 #include "tpe_internal.hpp"
 
+#ifndef TPE_LAT_SIDE
+#define TPE_LAT_SIDE 0  // 1: k_lattice on a side stream beside k_draw (fork / join)
+#endif
+
 using namespace tpe;
 
 struct tpe_engine {
@@ -549,16 +553,43 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
     erf_level = false;  // per-candidate quantized slots left after the lattice ones?
     for (int i = n_lat; i < n_level; ++i)
       erf_level |= kinds[i] == KIND_ERF_G || kinds[i] == KIND_ERF_L;
+    // the lattice needs only the fitted mixtures: it runs on a side stream
+    // beside the candidate draw (fork / join events; a parallel branch of the
+    // captured graph), and the scoring launch waits for it
     ScoreArgs la = base_args(p, n_sug);
+#if TPE_LAT_SIDE
+    hipStream_t sl = h->aux[0];
+    CKH(hipEventRecord(p->ev_fork, st));
+    CKH(hipStreamWaitEvent(sl, p->ev_fork, 0));
+#else
+    hipStream_t sl = st;
+#endif
     tpe_plan::Prof *pr = nullptr;
     if (p->prof_cap > 0 && p->prof[1].n < p->prof_cap) pr = &p->prof[1];
-    if (pr) CKH(hipEventRecord(pr->a[pr->n], st));
-    CKH(launch_lattice(la, lvl, n_lat, rmax, p->d_lat, st));
+    if (pr) CKH(hipEventRecord(pr->a[pr->n], sl));
+    CKH(launch_lattice(la, p->levels[level].data(), p->hps.data(), p->lat.data(), n_lat,
+                       p->d_lat, sl));
     if (pr) {
-      CKH(hipEventRecord(pr->b[pr->n], st));
+      CKH(hipEventRecord(pr->b[pr->n], sl));
       pr->pairs[pr->n] = (double)level;
       pr->n++;
     }
+#if TPE_LAT_SIDE
+    CKH(hipEventRecord(p->ev_join[0], sl));
+#endif
+  }
+  bool joined = !(TPE_LAT_SIDE && lat_level);
+  // log-sum-exp tiles: two candidate rows per lane, unless that leaves fewer
+  // than ~3 blocks per CU (then whole-block work units are few and coarse, and
+  // a CU with one more of them than its neighbours sets the launch time):
+  // one-row tiles double the count at the same per-pair arithmetic
+  {
+    int64_t lse_slots = 0;
+    for (int k : kinds) lse_slots += (k == KIND_LSE_G || k == KIND_LSE_L) ? 1 : 0;
+    const int64_t blocks2 = n_sug * lse_slots * ((n_cand + 127) / 128);
+    if (lse_slots > 0 && blocks2 < 3 * kNumCUs)
+      for (int &k : kinds)
+        k = k == KIND_LSE_G ? KIND_LSE_G1 : k == KIND_LSE_L ? KIND_LSE_L1 : k;
   }
   const int64_t budget = (int64_t)64 << 20;  // doubles
   const int64_t chunk = std::max<int64_t>(
@@ -591,6 +622,10 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
     CKH(launch_draw(a, table_draw, st));
     if (erf_level) CKH(launch_bucket(a, n_lat, p->d_cpos, st));
     a.cand_pos = erf_level ? p->d_cpos : nullptr;
+    if (!joined) {
+      CKH(hipStreamWaitEvent(st, p->ev_join[0], 0));
+      joined = true;
+    }
     rc = score_launch(h, p, a, erf_level, cn, st, true);
     if (rc) return rc;
     c0 += cn;

@@ -17,8 +17,11 @@ constexpr int kMaxLeaves = 160;  // numpy pairwise leaves per 8192 chunk (<=128)
 // scoring kernel instantiations (lpdf kinds)
 // KIND_LAT: a quantized hp scored on its value lattice (k_lattice) -- the
 // scoring launch only looks its candidates up (run_level picks it per level)
+// KIND_LSE_G1 / KIND_LSE_L1: the log-sum-exp kinds on one-row (64-candidate)
+// tiles, picked by run_level when two-row tiles would give the CUs too few,
+// unevenly shared blocks
 enum { KIND_LSE_G = 0, KIND_LSE_L = 1, KIND_ERF_G = 2, KIND_ERF_L = 3, KIND_CAT = 4,
-       KIND_LAT = 5 };
+       KIND_LAT = 5, KIND_LSE_G1 = 6, KIND_LSE_L1 = 7 };
 
 __host__ __device__ inline int score_kind(const tpe_hp &h) {
   if (h.family == TPE_CAT) return KIND_CAT;
@@ -29,10 +32,12 @@ __host__ __device__ inline int score_kind(const tpe_hp &h) {
 
 // candidate rows (per lane) of a scoring tile of the kind: 64 * rows candidates
 __host__ __device__ constexpr int tile_rows(int kind) {
-  return (kind == KIND_ERF_G || kind == KIND_ERF_L) ? 1
+  return (kind == KIND_ERF_G || kind == KIND_ERF_L || kind == KIND_LSE_G1 || kind == KIND_LSE_L1)
+             ? 1
          : (kind == KIND_CAT || kind == KIND_LAT) ? 4 : 2;
 }
 constexpr int kMaxGroups = 8;  // runs of one lpdf kind per launch (a level has <= 7)
+constexpr int kNumCUs = 256;   // MI355X (gfx950): 8 XCDs x 32 CUs
 
 struct MixInfo {
   int32_t K;        // components (categorical: upper)
@@ -162,11 +167,22 @@ hipError_t launch_prep(const tpe_hp *hps, int32_t n_hp, const double *mw,
                        Coef *coef, int64_t kcap, double *scratch,
                        hipStream_t st);
 hipError_t launch_score(const ScoreArgs &a, bool has_erf, hipStream_t st);
-// lpdf pairs of every lattice point of the n_lat hps lat_hps[] (one block of
-// kLatThreads per point; rmax = largest R), written to lat_out
-constexpr int kLatThreads = 1024;
-hipError_t launch_lattice(const ScoreArgs &a, const int32_t *lat_hps, int32_t n_lat, int64_t rmax,
-                          double2 *lat_out, hipStream_t st);
+// lpdf pairs of every lattice point of the first n_lat hps of a level
+// (hps_of_level[], host arrays; one block of kLatThreads per point, up to
+// kLatJobs hps per launch), written to lat_out
+constexpr int kLatThreads = 256;
+struct LatJob {  // one lattice hp of a k_lattice launch (kernel argument)
+  tpe_hp H;
+  LatInfo L;
+  int32_t hp;
+  int32_t pad;
+};
+constexpr int kLatJobs = 8;  // lattice hps per k_lattice launch
+struct LatJobs {
+  LatJob job[kLatJobs];
+};
+hipError_t launch_lattice(const ScoreArgs &a, const int32_t *hps_of_level, const tpe_hp *hps,
+                          const LatInfo *lat, int32_t n_lat, double2 *lat_out, hipStream_t st);
 constexpr int kTabCap = 2048;  // below-mixture components of the LDS draw table
 hipError_t launch_draw(const ScoreArgs &a, bool table, hipStream_t st);
 // slots slot_begin .. n_slots-1 (the lattice slots before them are not bucketed)

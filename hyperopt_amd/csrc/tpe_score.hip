@@ -26,6 +26,8 @@
 // when every candidate of the wave agrees.
 #include <math.h>
 
+#include <algorithm>
+
 #include "tpe_device.hpp"
 
 namespace tpe {
@@ -56,6 +58,12 @@ __device__ __forceinline__ void lse_merge(LseAcc &a, const LseAcc &b) {
 // below index them with wave-uniform addresses, so they compile to scalar
 // loads (s_load into SGPRs, one per wave, no LDS or VGPR traffic per lane).
 typedef const double __attribute__((address_space(4))) KDbl;
+
+// global (not flat) words of the in-launch tile hand-off
+typedef uint64_t __attribute__((address_space(1))) gu64;
+typedef uint32_t __attribute__((address_space(1))) gu32;
+__device__ __forceinline__ uint64_t dbits(double x) { return __builtin_bit_cast(uint64_t, x); }
+__device__ __forceinline__ double bitsd(uint64_t x) { return __builtin_bit_cast(double, x); }
 
 // a wave-uniform table pointer as a scalar (the compiler cannot always prove it)
 __device__ __forceinline__ KDbl *uniform_ptr(const Coef *p) {
@@ -312,10 +320,11 @@ template <int KIND, bool CENSUS>
 __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, int slot, int tile,
                                            int ntiles) {
   constexpr int KR = tile_rows(KIND);
-  constexpr bool LSE = KIND == KIND_LSE_G || KIND == KIND_LSE_L;
+  constexpr bool LSE = KIND == KIND_LSE_G || KIND == KIND_LSE_L || KIND == KIND_LSE_G1 ||
+                       KIND == KIND_LSE_L1;
   constexpr bool ERF = KIND == KIND_ERF_G || KIND == KIND_ERF_L;
   constexpr bool LAT = KIND == KIND_LAT;  // quantized, looked up on its value lattice
-  constexpr bool LOGN = KIND == KIND_LSE_L || KIND == KIND_ERF_L;
+  constexpr bool LOGN = KIND == KIND_LSE_L || KIND == KIND_LSE_L1 || KIND == KIND_ERF_L;
   const int s = blockIdx.y;
   const int hp = A.level_hps[slot];
   const tpe_hp H = A.hps[hp];
@@ -486,29 +495,33 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
   Partial *pbase = A.partial + ((int64_t)s * A.n_hp + hp) * A.pstride;
   int is_last = 0;
   if (lane == 0) {
-    pbase[tile] = Partial{best_s, best_v, best_i, 1, 0};
-    // publish the tile record, then take an arrival ticket (agent release /
-    // acquire, cdna_hip_programming.md Guideline 16 counter form)
+    // publish the tile record write-through (8-B agent-scope stores = sc1),
+    // drain, then take an arrival ticket; the last arriver reads every record
+    // with sc1 loads.  No L2 write-back / L1 invalidate fences (the
+    // MI355X_MICROARCH.md "valid forms" row: one lane stores and signals, the
+    // workgroup whose add returned last loads, all stores and loads sc1).
+    gu64 *rec = (gu64 *)(uintptr_t)(pbase + tile);
+    __hip_atomic_store(rec + 0, dbits(best_s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(rec + 1, dbits(best_v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(rec + 2, (uint64_t)best_i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    uint32_t *tk = A.ticket + (int64_t)s * A.n_hp + hp;
+    gu32 *tk = (gu32 *)(uintptr_t)(A.ticket + (int64_t)s * A.n_hp + hp);
     const uint32_t t = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     is_last = (t == (uint32_t)ntiles - 1) ? 1 : 0;
-    if (is_last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (is_last) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   is_last = __shfl(is_last, 0, 64);
   SSTAMP(2);
   if (!is_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the loads below the ticket
   double fs = NAN, fv = NAN;
   int64_t fi = -1;
   for (int i = lane; i < ntiles; i += 64) {
-    const Partial q = pbase[i];
-    if (better(q.score, q.index, fs, fi)) { fs = q.score; fv = q.value; fi = q.index; }
+    gu64 *rec = (gu64 *)(uintptr_t)(pbase + i);
+    const double qs = bitsd(__hip_atomic_load(rec + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const double qv = bitsd(__hip_atomic_load(rec + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const int64_t qi = (int64_t)__hip_atomic_load(rec + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (better(qs, qi, fs, fi)) { fs = qs; fv = qv; fi = qi; }
   }
   wave_best(fs, fv, fi);
   if (lane == 0) {
@@ -543,6 +556,8 @@ void k_score(ScoreArgs A) {
   switch (A.grp_kind[g]) {
     case KIND_LSE_G: score_tile<KIND_LSE_G, CENSUS>(A, sm, slot, tile, nt); break;
     case KIND_LSE_L: score_tile<KIND_LSE_L, CENSUS>(A, sm, slot, tile, nt); break;
+    case KIND_LSE_G1: score_tile<KIND_LSE_G1, CENSUS>(A, sm, slot, tile, nt); break;
+    case KIND_LSE_L1: score_tile<KIND_LSE_L1, CENSUS>(A, sm, slot, tile, nt); break;
     case KIND_ERF_G: if constexpr (ERFK) score_tile<KIND_ERF_G, CENSUS>(A, sm, slot, tile, nt); break;
     case KIND_ERF_L: if constexpr (ERFK) score_tile<KIND_ERF_L, CENSUS>(A, sm, slot, tile, nt); break;
     case KIND_LAT: score_tile<KIND_LAT, CENSUS>(A, sm, slot, tile, nt); break;
@@ -575,61 +590,97 @@ __device__ __forceinline__ void lattice_point(const ScoreArgs &A, const tpe_hp &
   const double *cb = reinterpret_cast<const double *>(A.coef + sb * A.kcap);
   const double *ca = reinterpret_cast<const double *>(A.coef + (sb + 1) * A.kcap);
   const int seg = (threadIdx.x & 63) & ~(kChunk - 1), j = threadIdx.x & (kChunk - 1);
-  for (int t0 = 0; t0 < kChunk * nch; t0 += blockDim.x) {
-    const int c = (t0 + (int)threadIdx.x) / kChunk;
-    double inc = 0.0;
-    if (c < nch) {
+  // kLatU rounds of the block at a time: every coefficient load of the batch
+  // is issued before the first erf, so one memory latency covers kLatU rounds
+  constexpr int kLatU = 4;
+  for (int t0 = 0; t0 < kChunk * nch; t0 += kLatU * (int)blockDim.x) {
+    double cx[kLatU], cy[kLatU], cw[kLatU];
+    bool ok[kLatU];
+#pragma unroll
+    for (int u = 0; u < kLatU; ++u) {
+      const int c = (t0 + u * (int)blockDim.x + (int)threadIdx.x) / kChunk;
       const bool above = c >= ncb;
       const int k = (above ? c - ncb : c) * kChunk + j;
-      if (k < (above ? ia.K : ib.K)) {
-        const double *cs = above ? ca : cb;
-        const double cx = cs[coef_off(k, 0)], cy = cs[coef_off(k, 1)];
-        const double zu = (ub - cx) * cy, zl = (lb - cx) * cy;
-        if (!erf_dead(zu, zl)) inc = erf_term<LOGN>(zu, zl, cs[coef_off(k, 2)]);
-      }
+      ok[u] = c < nch && k < (above ? ia.K : ib.K);
+      const double *cs = above ? ca : cb;
+      cx[u] = ok[u] ? cs[coef_off(k, 0)] : 0.0;
+      cy[u] = ok[u] ? cs[coef_off(k, 1)] : 0.0;
+      cw[u] = ok[u] ? cs[coef_off(k, 2)] : 0.0;
     }
-    double pc = 0.0;  // the chunk in component order
 #pragma unroll
-    for (int i = 0; i < kChunk; ++i) pc += __shfl(inc, seg + i, 64);
-    if (j == 0 && c < nch) csum[c] = pc;
+    for (int u = 0; u < kLatU; ++u) {
+      const int c = (t0 + u * (int)blockDim.x + (int)threadIdx.x) / kChunk;
+      double inc = 0.0;
+      if (ok[u]) {
+        const double zu = (ub - cx[u]) * cy[u], zl = (lb - cx[u]) * cy[u];
+        if (!erf_dead(zu, zl)) inc = erf_term<LOGN>(zu, zl, cw[u]);
+      }
+      double pc = 0.0;  // the chunk in component order
+#pragma unroll
+      for (int i = 0; i < kChunk; ++i) pc += __shfl(inc, seg + i, 64);
+      if (j == 0 && c < nch) csum[c] = pc;
+    }
   }
   __syncthreads();
-  if (threadIdx.x < 2) {
-    const int above = threadIdx.x;
+  // the "wave" totals: lane w (mod kWaves) of the first 2 * kWaves threads sums
+  // the chunks c = w, w + kWaves, ... of one mixture in order; lanes 0 / kWaves
+  // add the totals in wave order (erf_chunks / score_tile's merge)
+  const int t = threadIdx.x;
+  double sw = 0.0;
+  if (t < 2 * kWaves) {
+    const int above = t / kWaves, w = t % kWaves;
     const int c0 = above ? ncb : 0, n = above ? nca : ncb;
-    double tot = 0.0;
-    for (int w = 0; w < kWaves; ++w) {
-      double sw = 0.0;
-      for (int c = w; c < n; c += kWaves) sw += csum[c0 + c];
-      tot = w == 0 ? sw : tot + sw;
-    }
+    for (int c = w; c < n; c += kWaves) sw += csum[c0 + c];
+  }
+  double tot = sw;
+#pragma unroll
+  for (int w = 1; w < kWaves; ++w) {
+    const double v = __shfl(sw, (t & ~(kWaves - 1)) + w, 64);
+    tot = tot + v;
+  }
+  if (t == 0 || t == kWaves) {
+    const int above = t / kWaves;
     const double lp = log(tot) - (above ? ia.log_pacc : ib.log_pacc);
     double *o = reinterpret_cast<double *>(out + L.off + pt);
     o[above] = lp;
   }
 }
 
-__global__ __launch_bounds__(kLatThreads) void k_lattice(ScoreArgs A,
-                                                          const int32_t *__restrict__ lat_hps,
+// grid (lattice point, job): the jobs (hp descriptor + lattice) travel in the
+// kernel arguments, so a block's first memory accesses are its coefficients
+__global__ __launch_bounds__(kLatThreads) void k_lattice(ScoreArgs A, LatJobs J,
                                                           double2 *__restrict__ out) {
   extern __shared__ double csum[];  // [chunks of both mixtures]
-  const int hp = lat_hps[blockIdx.y];
-  const LatInfo L = A.lat_info[hp];
+  const LatJob &jb = J.job[blockIdx.y];
   const int64_t pt = blockIdx.x;
-  if (pt >= L.R) return;
-  const tpe_hp H = A.hps[hp];
-  if (H.family == TPE_LGMM) lattice_point<true>(A, H, hp, L, pt, csum, out);
-  else lattice_point<false>(A, H, hp, L, pt, csum, out);
+  if (pt >= jb.L.R) return;
+  if (jb.H.family == TPE_LGMM) lattice_point<true>(A, jb.H, jb.hp, jb.L, pt, csum, out);
+  else lattice_point<false>(A, jb.H, jb.hp, jb.L, pt, csum, out);
 }
 
-hipError_t launch_lattice(const ScoreArgs &a, const int32_t *lat_hps, int32_t n_lat, int64_t rmax,
-                          double2 *lat_out, hipStream_t st) {
-  if (n_lat <= 0 || rmax <= 0) return hipSuccess;
+hipError_t launch_lattice(const ScoreArgs &a, const int32_t *hps_of_level, const tpe_hp *hps,
+                          const LatInfo *lat, int32_t n_lat, double2 *lat_out, hipStream_t st) {
   const int64_t nch = 2 * ((a.kcap + kChunk - 1) / kChunk);
-  if (nch > kLatChunks || rmax > kLatMaxR) return hipErrorInvalidValue;
-  k_lattice<<<dim3((unsigned)rmax, (unsigned)n_lat), kLatThreads, (size_t)nch * sizeof(double),
-              st>>>(a, lat_hps, lat_out);
-  return hipGetLastError();
+  if (nch > kLatChunks) return hipErrorInvalidValue;
+  for (int32_t i0 = 0; i0 < n_lat; i0 += kLatJobs) {
+    LatJobs J{};
+    int64_t rmax = 0;
+    const int32_t n = std::min<int32_t>(kLatJobs, n_lat - i0);
+    for (int32_t i = 0; i < n; ++i) {
+      const int32_t hp = hps_of_level[i0 + i];
+      J.job[i].H = hps[hp];
+      J.job[i].L = lat[hp];
+      J.job[i].hp = hp;
+      rmax = std::max<int64_t>(rmax, lat[hp].R);
+    }
+    if (rmax > kLatMaxR) return hipErrorInvalidValue;
+    if (rmax <= 0) continue;
+    k_lattice<<<dim3((unsigned)rmax, (unsigned)n), kLatThreads, (size_t)nch * sizeof(double),
+                st>>>(a, J, lat_out);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 hipError_t launch_score(const ScoreArgs &a, bool has_erf, hipStream_t st) {
