@@ -10,11 +10,15 @@ of every hyperparameter, Philox candidate draws, below/above lpdf of every
 candidate against every component, EI argmax.  Default workload: BASELINE
 configs[1] = config 2 (20-D mixed space, 1000-trial history, 4096 candidates).
 
+--config cfg5 (BASELINE configs[4]: batched asynchronous suggestions x 1e6
+candidates, config 2's space and history): one step = one batch of --batch
+suggestions per rank in one engine call.
+
 Multi-GPU (torch.distributed.run, one rank per GPU): weak scaling, each rank
-serves its own asynchronous suggestion (distinct seed) on the shared history,
-no collective inside the timed region (batched suggestions shard with no data
-exchange; the in-suggest candidate sharding + RCCL max-loc path lives in
-hyperopt_amd/parallel.py and is exercised by --mode shard).
+serves its own asynchronous suggestions (distinct seeds) on the shared
+history, no collective inside the timed region (batched suggestions shard
+with no data exchange; the in-suggest candidate sharding + RCCL max-loc path
+is hyperopt_amd/parallel.py:ShardedSuggest, covered by tests/test_parallel.py).
 
 Prints ONE JSON line on rank 0.
 """
@@ -39,9 +43,9 @@ def build_workload(cfg):
     from hyperopt_amd import hp, rand, Trials
     from hyperopt_amd.base import Domain
     from hyperopt_amd.tpe import build_history
-    if cfg == 'cfg2':
+    if cfg in ('cfg2', 'cfg5'):
         dom = Domain(lambda x: 0.0, spaces.cfg2_space(hp))
-        n_hist, n_cand = 1000, 4096
+        n_hist, n_cand = 1000, (4096 if cfg == 'cfg2' else 1_000_000)
     elif cfg == 'cfg3':
         dom = Domain(lambda x: 0.0, spaces.cfg3_space(hp))
         n_hist, n_cand = 10000, 100000
@@ -103,7 +107,9 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=50)
     ap.add_argument('--warmup', type=int, default=10)
-    ap.add_argument('--config', default='cfg2', choices=['cfg2', 'cfg3', 'cfg4'])
+    ap.add_argument('--config', default='cfg2', choices=['cfg2', 'cfg3', 'cfg4', 'cfg5'])
+    ap.add_argument('--batch', type=int, default=0,
+                    help='suggestions per rank per step (default 1; cfg5: 16)')
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
     ap.add_argument('--n-cand', type=int, default=0,
                     help='override candidates per suggest (secondary measurements only)')
@@ -126,6 +132,7 @@ def main():
     dom, losses, vals, active, n_cand = build_workload(args.config)
     if args.n_cand:
         n_cand = args.n_cand
+    batch = args.batch or (16 if args.config == 'cfg5' else 1)
     hps, conds, pprior = dom.space.engine_tables()
     plan = E.Plan(eng, hps, conds, pprior, max_trials=losses.size)
     # history resident in HBM before the timed region
@@ -139,8 +146,8 @@ def main():
     def step(i):
         # fit + suggest in one engine call (a replayed hipGraph after the first
         # call of this shape); results stay device-resident in the plan
-        plan.fit_suggest([1_000_003 * rank + 17 * i + 7], n_cand, gamma=0.25, prior_weight=1.0,
-                         lf=25, fetch=False)
+        seeds = [1_000_003 * rank + 4099 * i + 17 * b + 7 for b in range(batch)]
+        plan.fit_suggest(seeds, n_cand, gamma=0.25, prior_weight=1.0, lf=25, fetch=False)
 
     for i in range(args.warmup):
         step(i)
@@ -180,7 +187,7 @@ def main():
     # A/B: the same steps with every quantized candidate scored on its own
     # (no value lattice), timed like the main region
     no_lat = None
-    if lat_launches:
+    if lat_launches and args.config == "cfg2":
         plan.set_lattice(False)
         for i in range(max(1, args.warmup)):
             step(i)
@@ -248,7 +255,7 @@ def main():
                 fp64_fma_peak_flops=eng.microbench(1), exp_f32_peak_per_s=eng.microbench(0),
                 erf_f64_peak_per_s=eng.microbench(2))
 
-    if lat_launches:
+    if lat_launches and args.config == "cfg2":
         roof['lattice'] = dict(
             kernel='k_lattice (bounded quantized hps: every lattice value j*q scored once per '
                    'suggest call, candidates look their lpdfs up in k_score; bit-identical)',
@@ -260,6 +267,8 @@ def main():
     if not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline(dom, losses, vals, active, n_cand if args.config == 'cfg2' else 4096,
                            args.cpu_seconds)
+        if args.config != 'cfg2':
+            cpu['sample'] += ' (config 2 suggests: the reference path cannot hold this config)'
 
     line = {
         'metric': 'EI candidates scored/sec (x components)',
@@ -278,10 +287,15 @@ def main():
             'workload': {'cfg2': 'config 2: 20-D mixed space, 1000-trial history, 4096 '
                                  'candidates/suggest', 'cfg3': 'config 3: 50-hp conditional, '
                                  '1e4 history, 1e5 candidates', 'cfg4': 'config 4: 100-D, 1e4 '
-                                 'history, 1e7 candidates'}[args.config],
+                                 'history, 1e7 candidates',
+                         'cfg5': 'config 5: batched asynchronous suggestions x 1e6 candidates '
+                                 '(config 2 space + 1000-trial history), %d suggestions per GPU '
+                                 'per step' % batch}[args.config],
+            'suggestions_per_step_per_gpu': batch,
             'candidates_per_suggest': n_cand,
-            'pairs_per_suggest': pairs_step,
-            'suggest_latency_ms': 1e3 * elapsed / args.steps,
+            'pairs_per_step': pairs_step,
+            'pairs_per_suggest': pairs_step / batch,
+            'suggest_latency_ms': 1e3 * elapsed / args.steps / batch,
             'parallelism': 'replicas' if world > 1 else 'single',
         },
         'roofline': roof,
