@@ -73,7 +73,10 @@ def build_workload(cfg):
 
 def cpu_baseline(dom, losses, vals, active, n_cand, budget_s):
     """The oracle (numpy restatement, pinned to the reference) timed on one
-    host core over whole config-2 suggests; pairs as the GPU counts them."""
+    host core over whole suggests of the bench's own space and history, with a
+    bounded candidate count (the reference path holds 8*n_c*K-byte temporaries,
+    so configs 3-5 cannot run at full n_c on the host); pairs as the GPU counts
+    them."""
     os.environ.setdefault('OPENBLAS_NUM_THREADS', '1')
     from oracle import tpe_oracle as O
     import spaces
@@ -96,9 +99,9 @@ def cpu_baseline(dom, losses, vals, active, n_cand, budget_s):
                     continue
                 pairs += len(dd['cand']) * (len(dd['below'][0]) + len(dd['above'][0]))
     return dict(value=pairs / t_total, unit='pairs/s', cores=1, kind='port',
-                sample='%d whole config-2 suggests (%d candidates each) through the oracle '
-                       '(numpy/scipy float64 restatement of tpe.py, bit-equal to reference '
-                       'fixtures), single thread, %.1f s' % (runs, n_cand, t_total),
+                sample='%d whole suggests of this config (%d candidates each) through the '
+                       'oracle (numpy/scipy float64 restatement of tpe.py, bit-equal to '
+                       'reference fixtures), single thread, %.1f s' % (runs, n_cand, t_total),
                 suggest_s=t_total / runs)
 
 
@@ -172,7 +175,7 @@ def main():
     # ---- profiled pass (after the timed region): HIP events on the engine
     # stream around every scoring launch, and the quantized-pair census
     n_prof = max(1, min(args.steps, 20))
-    plan.profile(n_prof)
+    plan.profile(n_prof * 64)   # event ring: every scoring launch of every profiled step
     for i in range(n_prof):
         step(args.warmup + args.steps + i)
     kinds = {}
@@ -265,10 +268,10 @@ def main():
             frac_of_erf_pair_peak=(lat_pairs / (lat_ms * 1e-3)) / erf_peak if lat_ms else None)
     cpu = None
     if not args.no_cpu_baseline and world == 1:
-        cpu = cpu_baseline(dom, losses, vals, active, n_cand if args.config == 'cfg2' else 4096,
-                           args.cpu_seconds)
-        if args.config != 'cfg2':
-            cpu['sample'] += ' (config 2 suggests: the reference path cannot hold this config)'
+        n_cpu = {'cfg2': n_cand, 'cfg3': 4096, 'cfg4': 128, 'cfg5': 4096}[args.config]
+        cpu = cpu_baseline(dom, losses, vals, active, n_cpu, args.cpu_seconds)
+        if n_cpu != n_cand:
+            cpu['sample'] += ' (bounded sample: %d of %d candidates per suggest)' % (n_cpu, n_cand)
 
     line = {
         'metric': 'EI candidates scored/sec (x components)',

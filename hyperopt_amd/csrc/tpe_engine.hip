@@ -400,23 +400,38 @@ int ensure_ext(tpe_engine *h, tpe_plan *p, size_t n) {
 // (consecutive slots of one kind form a group, tiles of 64 * tile_rows(kind)
 // candidates).  Returns the partial-record stride (max tiles per slot), or -1
 // when the slots are not grouped by kind.
+// Runs of equal-kind slots become groups of the 1-D scoring grid, emitted
+// heaviest kind first (per-candidate erf, then log-sum-exp, then the lattice /
+// categorical lookups): the dispatcher hands out the long blocks first and the
+// short ones fill the CUs that finish early.
 int32_t set_score_groups(ScoreArgs &a, const int *kinds, int n_slots, int64_t cn) {
   a.n_groups = 0;
   int32_t blocks = 0, pstride = 1;
-  for (int j = 0; j < n_slots;) {
-    int k = j;
-    while (k < n_slots && kinds[k] == kinds[j]) ++k;
-    if (a.n_groups == kMaxGroups) return -1;
-    const int g = a.n_groups++;
-    const int64_t tc = 64 * tile_rows(kinds[j]);
-    const int32_t nt = (int32_t)((std::max<int64_t>(cn, 0) + tc - 1) / tc);
-    a.grp_kind[g] = kinds[j];
-    a.grp_slot0[g] = j;
-    a.grp_tiles[g] = nt;
-    a.grp_block0[g] = blocks;
-    blocks += nt * (k - j);
-    pstride = std::max(pstride, nt);
-    j = k;
+  auto weight = [](int kind) {
+    switch (kind) {
+      case KIND_ERF_G: case KIND_ERF_L: return 0;
+      case KIND_LSE_G: case KIND_LSE_L: case KIND_LSE_G1: case KIND_LSE_L1: return 1;
+      case KIND_LAT: return 2;
+      default: return 3;
+    }
+  };
+  for (int pass = 0; pass < 4; ++pass) {
+    for (int j = 0; j < n_slots;) {
+      int k = j;
+      while (k < n_slots && kinds[k] == kinds[j]) ++k;
+      if (weight(kinds[j]) != pass) { j = k; continue; }
+      if (a.n_groups == kMaxGroups) return -1;
+      const int g = a.n_groups++;
+      const int64_t tc = 64 * tile_rows(kinds[j]);
+      const int32_t nt = (int32_t)((std::max<int64_t>(cn, 0) + tc - 1) / tc);
+      a.grp_kind[g] = kinds[j];
+      a.grp_slot0[g] = j;
+      a.grp_tiles[g] = nt;
+      a.grp_block0[g] = blocks;
+      blocks += nt * (k - j);
+      pstride = std::max(pstride, nt);
+      j = k;
+    }
   }
   a.grp_block0[a.n_groups] = blocks;
   return pstride;

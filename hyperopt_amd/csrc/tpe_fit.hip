@@ -431,6 +431,8 @@ __device__ __forceinline__ void block_np_sums(const double *const (&arr)[NA], in
         double r = 0.0;
         if (ln >= 8) {
           r = p[s];
+          // unrolled: the loads of a group are issued before its in-order adds
+#pragma unroll 4
           for (int i = 8 + s; i < body; i += 8) r += p[i];
         }
         r = r + __shfl_xor(r, 1, 64);

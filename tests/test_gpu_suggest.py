@@ -283,3 +283,20 @@ def test_value_lattice_bitwise_equals_per_candidate(name):
     plan.set_lattice(True)
     has_q = any(h.dist in ('quniform', 'qloguniform') for h in dom.space.hps)
     assert (ran > 0) == has_q, (ran, has_q)
+
+
+@pytest.mark.parametrize('name', ['cfg2', 'many_dists', 'cond', 'cfg3_small'])
+def test_fit_suggest_matches_fit_then_suggest(name):
+    """tpe_plan_fit_suggest (one engine call) equals fit() + suggest() bit for
+    bit on every test space, for single and batched suggestions (up to the 8
+    inline seeds) and candidate counts from n_EI=24 to beyond 8192."""
+    meta, d, dom, trials = _fixture_trials(name)
+    tpe.suggest([meta['new_id']], dom, trials, 7, n_EI_candidates=64)
+    plan = dom._tpe_state.plan
+    for seeds, n in [([3], 24), ([4], 4096), ([5, 6, 7], 2000), ([8], 8192), ([9], 8193),
+                     ([1, 2, 3, 4, 5, 6, 7, 8], 1024)]:
+        got = plan.fit_suggest(seeds, n)
+        plan.fit()
+        want = plan.suggest(seeds, n)
+        np.testing.assert_array_equal(got.view(np.uint8), want.view(np.uint8),
+                                      err_msg='%s %s %d' % (name, seeds, n))
