@@ -30,6 +30,22 @@ constexpr int kSortMax = 8192;  // candidates per bucketing chunk
 // the per-draw rejection sampler runs (!TAB), in a kernel of its own so the
 // table path keeps its small register footprint.
 constexpr int kDrawThreads = 256;
+// one table draw, out of line: inlined into the grid-stride loop below, the
+// inverse CDFs are specialised per descriptor branch and the kernel grows to
+// 256 VGPRs
+__device__ __attribute__((noinline)) double draw_table_ool(const tpe_hp *Hp, int K,
+                                                          const double *mu, const double *sg,
+                                                          const DrawTable *T, uint64_t seed,
+                                                          uint64_t gi, uint32_t stream) {
+  return draw_table(*Hp, K, mu, sg, *T, seed, gi, stream);
+}
+__device__ __attribute__((noinline)) double draw_one_ool(const tpe_hp *Hp, const MixInfo *I,
+                                                       const double *w, const double *mu,
+                                                       const double *sg, uint64_t seed,
+                                                       uint64_t gi, uint32_t stream) {
+  return draw_one(*Hp, *I, w, mu, sg, seed, gi, stream);
+}
+
 template <bool TAB>
 __global__ __launch_bounds__(kDrawThreads) void k_draw(ScoreArgs A) {
   __shared__ DrawTable T;
@@ -45,13 +61,16 @@ __global__ __launch_bounds__(kDrawThreads) void k_draw(ScoreArgs A) {
   if (tab) build_table(H, K, bw, bmu, bsg, T);
   const uint64_t seed = suggestion_seed(A, s);
   double *out = const_cast<double *>(A.cand) + (int64_t)s * A.cand_sstride + (int64_t)slot * A.n_cand;
-  // one candidate per thread (a grid-stride loop around the inlined inverse
-  // CDFs inflates the kernel to 256 VGPRs)
-  const int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (li < A.n_cand) {
+  // grid-stride over the chunk (not unrolled: an unrolled loop around the
+  // inlined inverse CDFs inflates the kernel to 256 VGPRs).  Large draws use
+  // several candidates per thread so one table build serves 2048 draws.
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+#pragma unroll 1
+  for (int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; li < A.n_cand; li += stride) {
     const uint64_t gi = (uint64_t)(A.cand_begin + li);
-    if constexpr (TAB) out[li] = tab ? draw_table(H, K, bmu, bsg, T, seed, gi, (uint32_t)hp) : NAN;
-    else out[li] = draw_one(H, ib, bw, bmu, bsg, seed, gi, (uint32_t)hp);
+    if constexpr (TAB)
+      out[li] = tab ? draw_table_ool(A.hps + hp, K, bmu, bsg, &T, seed, gi, (uint32_t)hp) : NAN;
+    else out[li] = draw_one_ool(A.hps + hp, A.info + sb, bw, bmu, bsg, seed, gi, (uint32_t)hp);
   }
 }
 
@@ -294,7 +313,10 @@ bool is_draw_kernel_fn(const void *f) {
 
 hipError_t launch_draw(const ScoreArgs &a, bool table, hipStream_t st) {
   if (a.n_slots <= 0 || a.n_suggest <= 0 || a.n_cand <= 0) return hipSuccess;
-  const unsigned gx = (unsigned)((a.n_cand + kDrawThreads - 1) / kDrawThreads);
+  // one candidate per thread while that leaves the grid short (latency), up
+  // to 8 per thread for large chunks (the per-block table build amortised)
+  const int64_t per = a.n_cand * a.n_slots * a.n_suggest >= ((int64_t)1 << 22) ? 8 : 1;
+  const unsigned gx = (unsigned)((a.n_cand + kDrawThreads * per - 1) / (kDrawThreads * per));
   if (table) k_draw<true><<<dim3(gx, a.n_slots, a.n_suggest), kDrawThreads, 0, st>>>(a);
   else k_draw<false><<<dim3(gx, a.n_slots, a.n_suggest), kDrawThreads, 0, st>>>(a);
   return hipGetLastError();

@@ -300,3 +300,22 @@ def test_fit_suggest_matches_fit_then_suggest(name):
         want = plan.suggest(seeds, n)
         np.testing.assert_array_equal(got.view(np.uint8), want.view(np.uint8),
                                       err_msg='%s %s %d' % (name, seeds, n))
+
+
+def test_large_draw_grid_stride_matches_one_per_thread():
+    """Large draws take 8 candidates per thread (grid-stride k_draw), small
+    ones one; candidates are counter-based, so a 2^18-candidate suggest
+    (strided path) must equal the merge of two chunks drawn one per thread."""
+    torch = pytest.importorskip('torch')
+    meta, d, dom, trials = _fixture_trials('cfg2')
+    tpe.suggest([meta['new_id']], dom, trials, 7, n_EI_candidates=64)
+    plan = dom._tpe_state.plan
+    n, cut = 1 << 18, 100_000
+    assert n * len(dom.space.labels) >= 1 << 22 and (n - cut) * len(dom.space.labels) < 1 << 22
+    full = plan.suggest([13], n)
+    parts = [plan.suggest([13], cut, cand_begin=0), plan.suggest([13], n - cut, cand_begin=cut)]
+    raw = torch.from_numpy(np.stack(parts).view(np.uint8).reshape(-1).copy()).cuda()
+    merged = plan.merge(raw.data_ptr(), world=2, level=0)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(merged['index'], full['index'])
+    np.testing.assert_array_equal(merged['value'], full['value'])
