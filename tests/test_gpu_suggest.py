@@ -319,3 +319,19 @@ def test_large_draw_grid_stride_matches_one_per_thread():
     torch.cuda.synchronize()
     np.testing.assert_array_equal(merged['index'], full['index'])
     np.testing.assert_array_equal(merged['value'], full['value'])
+
+
+def test_graph_replay_in_child_process():
+    """The opt-in hipGraph replay (TPE_GRAPH=1, read once per process) with the
+    per-call seed patches of the draw nodes -- k_draw, or k_lattice's fused
+    draw rows -- equals eager fit() + suggest(), in a child process."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path.insert(0, 'tests'); import test_gpu_suggest as t; "
+            "t.test_fit_suggest_graph_replay_matches_eager(); "
+            "[t.test_fit_suggest_matches_fit_then_suggest(n) for n in ('cfg2', 'cond')]; print('OK')")
+    r = subprocess.run([sys.executable, '-c', code], cwd=root, env=dict(os.environ, TPE_GRAPH='1'),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and 'OK' in r.stdout, (r.stdout[-1000:], r.stderr[-3000:])
