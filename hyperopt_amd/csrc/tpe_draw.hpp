@@ -214,4 +214,40 @@ __device__ __forceinline__ uint64_t suggestion_seed(const ScoreArgs &A, int s) {
   return v;
 }
 
+// one table draw, out of line: inlined into the grid-stride loop below, the
+// inverse CDFs are specialised per descriptor branch and the kernel grows to
+// 256 VGPRs
+template <int CAP>
+__device__ __attribute__((noinline)) double draw_table_ool(const tpe_hp *Hp, int K,
+                                                          const double *mu, const double *sg,
+                                                          const DrawTableT<CAP> *T, uint64_t seed,
+                                                          uint64_t gi, uint32_t stream) {
+  return draw_table(*Hp, K, mu, sg, *T, seed, gi, stream);
+}
+
+// One draw block (k_draw<true>, or a draw row of the fused k_lattice): the
+// below mixture's table of (suggestion s, level slot) in LDS, then a
+// grid-stride pass over the chunk's candidates bx * blockDim + t (+ stride).
+// Large draws use several candidates per thread so one table build serves
+// 2048 draws.  K > CAP (not routed here by the host) draws NaN.
+template <int CAP>
+__device__ void draw_block(const ScoreArgs &A, int bx, int slot, int s, DrawTableT<CAP> &T,
+                           int64_t stride) {
+  const int hp = A.level_hps[slot];
+  const tpe_hp H = A.hps[hp];
+  if (!hp_active(H, A.results + (int64_t)s * A.n_hp, A.cond_parent, A.cond_branch)) return;
+  const int64_t sb = 2 * (int64_t)hp;
+  const double *bw = A.mw + sb * A.kcap, *bmu = A.mmu + sb * A.kcap, *bsg = A.msig + sb * A.kcap;
+  const int K = A.info[sb].K;
+  const bool tab = K >= 1 && K <= CAP;
+  if (tab) build_table(H, K, bw, bmu, bsg, T);
+  const uint64_t seed = suggestion_seed(A, s);
+  double *out = const_cast<double *>(A.cand) + (int64_t)s * A.cand_sstride + (int64_t)slot * A.n_cand;
+#pragma unroll 1
+  for (int64_t li = (int64_t)bx * blockDim.x + threadIdx.x; li < A.n_cand; li += stride)
+    out[li] = tab ? draw_table_ool<CAP>(A.hps + hp, K, bmu, bsg, &T, seed,
+                                        (uint64_t)(A.cand_begin + li), (uint32_t)hp)
+                  : NAN;
+}
+
 }  // namespace tpe

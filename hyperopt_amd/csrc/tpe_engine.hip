@@ -563,11 +563,23 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
   const bool lat_level = n_lat > 0 && p->lattice_on && rmax <= n_cand * n_sug &&
                          2 * ((p->kcap + 15) / 16) <= (int64_t)kLatChunks;
   if (!lat_level) n_lat = 0;
+  const int64_t budget = (int64_t)64 << 20;  // doubles
+  const int64_t chunk = std::max<int64_t>(
+      1, std::min<int64_t>(std::max<int64_t>(n_cand, 1),
+                           budget / std::max<int64_t>(1, n_sug * n_level)));
+  // a small one-chunk draw whose tables fit kFuseTab runs in extra blocks of
+  // the lattice launch (both only need the fitted mixtures): one launch less
+  // and the draw hidden behind the lattice points
+  const bool fuse_draw = !TPE_LAT_SIDE && lat_level && n_lat <= kLatJobs && table_draw &&
+                         kmax <= kFuseTab && chunk >= n_cand &&
+                         n_cand * n_sug * n_level < ((int64_t)1 << 22);
   if (lat_level) {
     for (int i = 0; i < n_lat; ++i) kinds[i] = KIND_LAT;
     erf_level = false;  // per-candidate quantized slots left after the lattice ones?
     for (int i = n_lat; i < n_level; ++i)
       erf_level |= kinds[i] == KIND_ERF_G || kinds[i] == KIND_ERF_L;
+  }
+  if (lat_level && !fuse_draw) {
     // the lattice needs only the fitted mixtures: it runs on a side stream
     // beside the candidate draw (fork / join events; a parallel branch of the
     // captured graph), and the scoring launch waits for it
@@ -606,10 +618,6 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
       for (int &k : kinds)
         k = k == KIND_LSE_G ? KIND_LSE_G1 : k == KIND_LSE_L ? KIND_LSE_L1 : k;
   }
-  const int64_t budget = (int64_t)64 << 20;  // doubles
-  const int64_t chunk = std::max<int64_t>(
-      1, std::min<int64_t>(std::max<int64_t>(n_cand, 1),
-                           budget / std::max<int64_t>(1, n_sug * n_level)));
   int64_t c0 = 0;
   do {
     const int64_t cn = std::min(chunk, n_cand - c0);
@@ -634,7 +642,20 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
     a.cand_slot0 = 0;
     for (int i = 0; i < kInlineSeeds && i < n_sug; ++i) a.seed_inline[i] = p->h_seeds[i];
     a.n_inline_seeds = (int32_t)std::min<int64_t>(n_sug, kInlineSeeds);
-    CKH(launch_draw(a, table_draw, st));
+    if (fuse_draw) {
+      tpe_plan::Prof *pr = nullptr;
+      if (p->prof_cap > 0 && p->prof[1].n < p->prof_cap) pr = &p->prof[1];
+      if (pr) CKH(hipEventRecord(pr->a[pr->n], st));
+      CKH(launch_lattice_draw(a, p->levels[level].data(), p->hps.data(), p->lat.data(), n_lat,
+                              p->d_lat, st));
+      if (pr) {
+        CKH(hipEventRecord(pr->b[pr->n], st));
+        pr->pairs[pr->n] = (double)level;
+        pr->n++;
+      }
+    } else {
+      CKH(launch_draw(a, table_draw, st));
+    }
     if (erf_level) CKH(launch_bucket(a, n_lat, p->d_cpos, st));
     a.cand_pos = erf_level ? p->d_cpos : nullptr;
     if (!joined) {
@@ -1124,7 +1145,7 @@ int capture_step(tpe_engine *h, tpe_plan *p, int32_t nb, double prior_weight, in
       p->fit_nodes.push_back(nd);
       p->fit_params.push_back(kp);
       p->fit_args0.push_back(*static_cast<const FitArgs *>(kp.kernelParams[0]));
-    } else if (is_draw_kernel_fn(kp.func)) {
+    } else if (is_draw_kernel_fn(kp.func) || kp.func == lattice_draw_kernel_fn()) {
       p->draw_nodes.push_back(nd);
       p->draw_params.push_back(kp);
       p->draw_args0.push_back(*static_cast<const ScoreArgs *>(kp.kernelParams[0]));
@@ -1155,8 +1176,15 @@ int launch_step(tpe_engine *h, tpe_plan *p, int32_t nb, const uint64_t *seeds, i
     ScoreArgs da = p->draw_args0[i];
     for (int64_t j = 0; j < n_sug; ++j) da.seed_inline[j] = seeds[j];
     da.n_inline_seeds = (int32_t)n_sug;
-    void *args[1] = {&da};
     hipKernelNodeParams kp = p->draw_params[i];
+    // k_lattice<true> (fused draw) also takes its jobs and output pointer
+    LatJobs jobs{};
+    double2 *lat_out = nullptr;
+    void *args[3] = {&da, &jobs, &lat_out};
+    if (kp.func == lattice_draw_kernel_fn()) {
+      jobs = *static_cast<const LatJobs *>(kp.kernelParams[1]);
+      lat_out = *static_cast<double2 *const *>(kp.kernelParams[2]);
+    }
     kp.kernelParams = args;
     kp.extra = nullptr;
     CKH(hipGraphExecKernelNodeSetParams(p->graph_exec, p->draw_nodes[i], &kp));

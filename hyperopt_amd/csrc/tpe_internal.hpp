@@ -162,6 +162,7 @@ hipError_t launch_split(const FitArgs &a, uint8_t *below, hipStream_t st);
 hipError_t launch_fit(const FitArgs &a, int32_t n_hp, hipStream_t st);
 const void *fit_kernel_fn();               // k_fit's host stub (graph node lookup)
 bool is_draw_kernel_fn(const void *f);     // one of k_draw's host stubs
+const void *lattice_draw_kernel_fn();      // k_lattice<true> (lattice + fused draw)
 hipError_t launch_prep(const tpe_hp *hps, int32_t n_hp, const double *mw,
                        const double *mmu, const double *msig, MixInfo *info,
                        Coef *coef, int64_t kcap, double *scratch,
@@ -180,9 +181,22 @@ struct LatJob {  // one lattice hp of a k_lattice launch (kernel argument)
 constexpr int kLatJobs = 8;  // lattice hps per k_lattice launch
 struct LatJobs {
   LatJob job[kLatJobs];
+  // fused candidate draw (launch_lattice_draw): grid rows y >= n_jobs are
+  // draw blocks d = (y - n_jobs) * gridDim.x + x of a (draw_gx, slots, S) grid
+  int32_t n_jobs;
+  int32_t draw_gx;
+  int32_t draw_blocks;
+  int32_t pad;
 };
+constexpr int kFuseTab = 32;  // below K of a draw fused into k_lattice (LDS table)
 hipError_t launch_lattice(const ScoreArgs &a, const int32_t *hps_of_level, const tpe_hp *hps,
                           const LatInfo *lat, int32_t n_lat, double2 *lat_out, hipStream_t st);
+// the same lattice launch with the level's candidate draw (draw args `a`, one
+// candidate per thread, every below K <= kFuseTab) in extra blocks of it: the
+// two only need the fitted mixtures and run side by side
+hipError_t launch_lattice_draw(const ScoreArgs &a, const int32_t *hps_of_level, const tpe_hp *hps,
+                               const LatInfo *lat, int32_t n_lat, double2 *lat_out,
+                               hipStream_t st);
 constexpr int kTabCap = 2048;  // below-mixture components of the LDS draw table
 hipError_t launch_draw(const ScoreArgs &a, bool table, hipStream_t st);
 // slots slot_begin .. n_slots-1 (the lattice slots before them are not bucketed)

@@ -30,15 +30,6 @@ constexpr int kSortMax = 8192;  // candidates per bucketing chunk
 // the per-draw rejection sampler runs (!TAB), in a kernel of its own so the
 // table path keeps its small register footprint.
 constexpr int kDrawThreads = 256;
-// one table draw, out of line: inlined into the grid-stride loop below, the
-// inverse CDFs are specialised per descriptor branch and the kernel grows to
-// 256 VGPRs
-__device__ __attribute__((noinline)) double draw_table_ool(const tpe_hp *Hp, int K,
-                                                          const double *mu, const double *sg,
-                                                          const DrawTable *T, uint64_t seed,
-                                                          uint64_t gi, uint32_t stream) {
-  return draw_table(*Hp, K, mu, sg, *T, seed, gi, stream);
-}
 __device__ __attribute__((noinline)) double draw_one_ool(const tpe_hp *Hp, const MixInfo *I,
                                                        const double *w, const double *mu,
                                                        const double *sg, uint64_t seed,
@@ -48,29 +39,23 @@ __device__ __attribute__((noinline)) double draw_one_ool(const tpe_hp *Hp, const
 
 template <bool TAB>
 __global__ __launch_bounds__(kDrawThreads) void k_draw(ScoreArgs A) {
-  __shared__ DrawTable T;
-  const int slot = blockIdx.y, s = blockIdx.z;
-  const int hp = A.level_hps[slot];
-  const tpe_hp H = A.hps[hp];
-  if (!hp_active(H, A.results + (int64_t)s * A.n_hp, A.cond_parent, A.cond_branch)) return;
-  const int64_t sb = 2 * (int64_t)hp;
-  const MixInfo ib = A.info[sb];
-  const double *bw = A.mw + sb * A.kcap, *bmu = A.mmu + sb * A.kcap, *bsg = A.msig + sb * A.kcap;
-  const int K = ib.K;
-  const bool tab = TAB && K >= 1 && K <= kTabCap;
-  if (tab) build_table(H, K, bw, bmu, bsg, T);
-  const uint64_t seed = suggestion_seed(A, s);
-  double *out = const_cast<double *>(A.cand) + (int64_t)s * A.cand_sstride + (int64_t)slot * A.n_cand;
-  // grid-stride over the chunk (not unrolled: an unrolled loop around the
-  // inlined inverse CDFs inflates the kernel to 256 VGPRs).  Large draws use
-  // several candidates per thread so one table build serves 2048 draws.
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  if constexpr (TAB) {
+    __shared__ DrawTable T;
+    draw_block<kTabCap>(A, blockIdx.x, blockIdx.y, blockIdx.z, T, (int64_t)gridDim.x * blockDim.x);
+  } else {
+    const int slot = blockIdx.y, s = blockIdx.z;
+    const int hp = A.level_hps[slot];
+    const tpe_hp H = A.hps[hp];
+    if (!hp_active(H, A.results + (int64_t)s * A.n_hp, A.cond_parent, A.cond_branch)) return;
+    const int64_t sb = 2 * (int64_t)hp;
+    const double *bw = A.mw + sb * A.kcap, *bmu = A.mmu + sb * A.kcap, *bsg = A.msig + sb * A.kcap;
+    const uint64_t seed = suggestion_seed(A, s);
+    double *out = const_cast<double *>(A.cand) + (int64_t)s * A.cand_sstride + (int64_t)slot * A.n_cand;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
 #pragma unroll 1
-  for (int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; li < A.n_cand; li += stride) {
-    const uint64_t gi = (uint64_t)(A.cand_begin + li);
-    if constexpr (TAB)
-      out[li] = tab ? draw_table_ool(A.hps + hp, K, bmu, bsg, &T, seed, gi, (uint32_t)hp) : NAN;
-    else out[li] = draw_one_ool(A.hps + hp, A.info + sb, bw, bmu, bsg, seed, gi, (uint32_t)hp);
+    for (int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; li < A.n_cand; li += stride)
+      out[li] = draw_one_ool(A.hps + hp, A.info + sb, bw, bmu, bsg, seed,
+                             (uint64_t)(A.cand_begin + li), (uint32_t)hp);
   }
 }
 

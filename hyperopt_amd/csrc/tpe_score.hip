@@ -29,6 +29,7 @@
 #include <algorithm>
 
 #include "tpe_device.hpp"
+#include "tpe_draw.hpp"
 
 namespace tpe {
 
@@ -648,9 +649,23 @@ __device__ __forceinline__ void lattice_point(const ScoreArgs &A, const tpe_hp &
 
 // grid (lattice point, job): the jobs (hp descriptor + lattice) travel in the
 // kernel arguments, so a block's first memory accesses are its coefficients
+// DRAW: rows y >= J.n_jobs draw the level's candidates instead (k_draw<true>'s
+// blocks, table of <= kFuseTab components in the same dynamic LDS)
+template <bool DRAW>
 __global__ __launch_bounds__(kLatThreads) void k_lattice(ScoreArgs A, LatJobs J,
                                                           double2 *__restrict__ out) {
   extern __shared__ double csum[];  // [chunks of both mixtures]
+  if constexpr (DRAW) {
+    if ((int)blockIdx.y >= J.n_jobs) {
+      const int d = ((int)blockIdx.y - J.n_jobs) * (int)gridDim.x + (int)blockIdx.x;
+      if (d >= J.draw_blocks) return;
+      const int per_s = J.draw_gx * A.n_slots;
+      draw_block<kFuseTab>(A, d % J.draw_gx, (d % per_s) / J.draw_gx, d / per_s,
+                           *reinterpret_cast<DrawTableT<kFuseTab> *>(csum),
+                           (int64_t)J.draw_gx * blockDim.x);
+      return;
+    }
+  }
   const LatJob &jb = J.job[blockIdx.y];
   const int64_t pt = blockIdx.x;
   if (pt >= jb.L.R) return;
@@ -675,12 +690,44 @@ hipError_t launch_lattice(const ScoreArgs &a, const int32_t *hps_of_level, const
     }
     if (rmax > kLatMaxR) return hipErrorInvalidValue;
     if (rmax <= 0) continue;
-    k_lattice<<<dim3((unsigned)rmax, (unsigned)n), kLatThreads, (size_t)nch * sizeof(double),
-                st>>>(a, J, lat_out);
+    J.n_jobs = n;
+    k_lattice<false><<<dim3((unsigned)rmax, (unsigned)n), kLatThreads,
+                       (size_t)nch * sizeof(double), st>>>(a, J, lat_out);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
+}
+
+const void *lattice_draw_kernel_fn() { return reinterpret_cast<const void *>(&k_lattice<true>); }
+
+hipError_t launch_lattice_draw(const ScoreArgs &a, const int32_t *hps_of_level, const tpe_hp *hps,
+                               const LatInfo *lat, int32_t n_lat, double2 *lat_out,
+                               hipStream_t st) {
+  static_assert(kLatThreads == 256, "draw rows run k_draw's 256-thread blocks");
+  const int64_t nch = 2 * ((a.kcap + kChunk - 1) / kChunk);
+  if (nch > kLatChunks || n_lat < 1 || n_lat > kLatJobs || a.n_cand <= 0) return hipErrorInvalidValue;
+  LatJobs J{};
+  int64_t rmax = 0;
+  for (int32_t i = 0; i < n_lat; ++i) {
+    const int32_t hp = hps_of_level[i];
+    J.job[i].H = hps[hp];
+    J.job[i].L = lat[hp];
+    J.job[i].hp = hp;
+    rmax = std::max<int64_t>(rmax, lat[hp].R);
+  }
+  if (rmax > kLatMaxR || rmax <= 0) return hipErrorInvalidValue;
+  const int64_t gx = (a.n_cand + kLatThreads - 1) / kLatThreads;
+  const int64_t draws = gx * a.n_slots * a.n_suggest;
+  if (draws > ((int64_t)1 << 30)) return hipErrorInvalidValue;
+  J.n_jobs = n_lat;
+  J.draw_gx = (int32_t)gx;
+  J.draw_blocks = (int32_t)draws;
+  const int64_t rows = (draws + rmax - 1) / rmax;
+  const size_t lds = std::max<size_t>((size_t)nch * sizeof(double), sizeof(DrawTableT<kFuseTab>));
+  k_lattice<true><<<dim3((unsigned)rmax, (unsigned)(n_lat + rows)), kLatThreads, lds, st>>>(
+      a, J, lat_out);
+  return hipGetLastError();
 }
 
 hipError_t launch_score(const ScoreArgs &a, bool has_erf, hipStream_t st) {
