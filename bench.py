@@ -261,7 +261,8 @@ def main():
     if lat_launches and args.config == "cfg2":
         roof['lattice'] = dict(
             kernel='k_lattice (bounded quantized hps: every lattice value j*q scored once per '
-                   'suggest call, candidates look their lpdfs up in k_score; bit-identical)',
+                   'suggest call, candidates look their lpdfs up in k_score; bit-identical; for '
+                   'small draws the launch also carries the candidate-draw blocks, timed with it)',
             avg_launch_ms=lat_ms, launches_per_step=lat_launches / n_prof,
             pairs_per_launch=lat_pairs,
             erf_pair_rate_per_s=lat_pairs / (lat_ms * 1e-3) if lat_ms else None,
