@@ -11,6 +11,7 @@ from .base import (STATUS_STRINGS, STATUS_NEW, STATUS_RUNNING, STATUS_SUSPENDED,
                    STATUS_OK, STATUS_FAIL, JOB_STATES, JOB_STATE_NEW, JOB_STATE_RUNNING,
                    JOB_STATE_DONE, JOB_STATE_ERROR, Ctrl, Trials, trials_from_docs, Domain)
 from .fmin import fmin, fmin_pass_expr_memo_ctrl, FMinIter, partial, space_eval  # noqa: F401
+from .workers import ThreadTrials  # noqa: F401
 from .expr import scope  # noqa: F401
 from . import hp, rand, tpe  # noqa: F401
 

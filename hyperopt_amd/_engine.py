@@ -39,7 +39,7 @@ EXPORTS = (
     'tpe_plan_suggest', 'tpe_plan_merge', 'tpe_plan_score_candidates', 'tpe_plan_last_stats',
     'tpe_plan_profile', 'tpe_plan_profile_read', 'tpe_microbench', 'tpe_plan_get_results',
     'tpe_plan_results_device', 'tpe_plan_census', 'tpe_plan_fit_suggest',
-    'tpe_plan_set_lattice',
+    'tpe_plan_set_lattice', 'tpe_plan_update_history',
 )
 
 
@@ -128,6 +128,8 @@ def load_library(path: str = LIB_PATH):
             'tpe_plan_destroy': (C.c_int, [vp]),
             'tpe_plan_num_levels': (C.c_int, [vp, C.POINTER(i32)]),
             'tpe_plan_set_history': (C.c_int, [vp, vp, vp, vp, i64, i32, vp]),
+            'tpe_plan_update_history': (C.c_int, [vp, i64, i64, i64, vp, vp, i64, i64, vp, i32,
+                                                  vp]),
             'tpe_plan_fit': (C.c_int, [vp, dbl, i32, dbl, i32, vp]),
             'tpe_plan_get_mixture': (C.c_int, [vp, i32, i32, _D, _D, _D, i64, C.POINTER(i64)]),
             'tpe_plan_suggest': (C.c_int, [vp, C.POINTER(u64), i64, i64, i64, i32, vp, i32, vp]),
@@ -333,23 +335,40 @@ class Plan(object):
         except Exception:
             pass
 
-    def set_history(self, losses, vals, active, on_device=False, stream=None):
-        """losses[n], vals[n_hp, n] float64, active[n_hp, n] uint8.  Host numpy
-        arrays, or (on_device=True) raw device pointers (ints)."""
-        e = self.engine
-        if on_device:
-            lp, vp, ap, n = losses, vals, active, None
-            raise NotImplementedError('use set_history_device')
+    def set_history(self, losses, vals, active, stream=None):
+        """Whole history from host arrays: losses[n], vals[n_hp, n] float64,
+        active[n_hp, n] uint8."""
         losses = _f64(losses)
         vals = _f64(vals)
         active = np.ascontiguousarray(active, dtype=np.uint8)
         n = losses.size
         assert vals.shape == (self.n_hp, n) and active.shape == (self.n_hp, n)
-        self._hist = (losses, vals, active)
+        self.update_history(n, 0, vals, active, n, 0, losses, stream=stream)
+
+    def update_history(self, n, row0, vals, active, ld, loss0, losses, stream=None):
+        """Incremental history (tpe_plan_update_history): rows [row0, n) of
+        the host columns vals[n_hp, ld] / active[n_hp, ld] (C-contiguous) and
+        losses[loss0:n]; rows below row0 stay as the device has them."""
+        e = self.engine
+        if n > self.max_trials:
+            raise ValueError('history of %d trials exceeds the plan capacity %d'
+                             % (n, self.max_trials))
+        if vals.dtype != np.float64 or active.dtype != np.uint8 or \
+                not vals.flags.c_contiguous or not active.flags.c_contiguous or \
+                vals.shape != (self.n_hp, ld) or active.shape != (self.n_hp, ld):
+            raise ValueError('history columns must be C-contiguous [n_hp, ld] f64 / u8')
+        losses = np.asarray(losses)
+        if losses.dtype != np.float64 or not losses.flags.c_contiguous:
+            raise ValueError('losses must be C-contiguous float64')
+        nr = n - row0
+        vp = vals.ctypes.data + 8 * row0 if nr > 0 else None
+        ap = active.ctypes.data + row0 if nr > 0 else None
+        lp = losses.ctypes.data + 8 * loss0 if loss0 < n else None
+        self._hist = (vals, active, losses)   # keep the host memory alive
         with e.lock:
-            e.check(e.lib.tpe_plan_set_history(self.p, losses.ctypes.data, vals.ctypes.data,
-                                               active.ctypes.data, n, 0, stream))
-        self.n = n
+            e.check(e.lib.tpe_plan_update_history(self.p, int(n), int(row0), int(nr), vp, ap,
+                                                  int(ld), int(loss0), lp, 0, stream))
+        self.n = int(n)
 
     def set_history_device(self, losses_ptr, vals_ptr, active_ptr, n, stream=None):
         e = self.engine

@@ -225,11 +225,20 @@ __device__ __attribute__((noinline)) double draw_table_ool(const tpe_hp *Hp, int
   return draw_table(*Hp, K, mu, sg, *T, seed, gi, stream);
 }
 
+// the per-draw rejection sampler, out of line (small register footprint for
+// the table kernels that fall back to it)
+__device__ __attribute__((noinline)) inline double draw_one_ool(
+    const tpe_hp *Hp, const MixInfo *I, const double *w, const double *mu, const double *sg,
+    uint64_t seed, uint64_t gi, uint32_t stream) {
+  return draw_one(*Hp, *I, w, mu, sg, seed, gi, stream);
+}
+
 // One draw block (k_draw<true>, or a draw row of the fused k_lattice): the
 // below mixture's table of (suggestion s, level slot) in LDS, then a
 // grid-stride pass over the chunk's candidates bx * blockDim + t (+ stride).
 // Large draws use several candidates per thread so one table build serves
-// 2048 draws.  K > CAP (not routed here by the host) draws NaN.
+// 2048 draws.  K > CAP (a stale host routing decision) falls back to the
+// rejection sampler: the same distribution, never a silent NaN.
 template <int CAP>
 __device__ void draw_block(const ScoreArgs &A, int bx, int slot, int s, DrawTableT<CAP> &T,
                            int64_t stride) {
@@ -247,7 +256,8 @@ __device__ void draw_block(const ScoreArgs &A, int bx, int slot, int s, DrawTabl
   for (int64_t li = (int64_t)bx * blockDim.x + threadIdx.x; li < A.n_cand; li += stride)
     out[li] = tab ? draw_table_ool<CAP>(A.hps + hp, K, bmu, bsg, &T, seed,
                                         (uint64_t)(A.cand_begin + li), (uint32_t)hp)
-                  : NAN;
+                  : draw_one_ool(A.hps + hp, A.info + sb, bw, bmu, bsg, seed,
+                                 (uint64_t)(A.cand_begin + li), (uint32_t)hp);
 }
 
 }  // namespace tpe

@@ -99,10 +99,11 @@ struct tpe_plan {
     int32_t lf = 0;
     int64_t n_sug = 0, n_cand = 0;
     void *stream = nullptr;
-    bool table = false;
+    bool table = false;  // below mixtures fit the LDS draw table (kTabCap)
+    bool fuse = false;   // ... and the fused k_lattice draw rows' table (kFuseTab)
     bool operator==(const StepKey &o) const {
       return prior_weight == o.prior_weight && lf == o.lf && n_sug == o.n_sug &&
-             n_cand == o.n_cand && stream == o.stream && table == o.table;
+             n_cand == o.n_cand && stream == o.stream && table == o.table && fuse == o.fuse;
     }
   };
   StepKey graph_key, pending_key;
@@ -498,6 +499,7 @@ FitArgs fit_args(tpe_plan *p, int32_t n_below, double prior_weight, int32_t lf) 
   a.active = p->d_active;
   a.losses = p->d_losses;
   a.n = p->n;
+  a.ld = p->ncap;
   a.n_below = n_below;
   a.lf = lf;
   a.prior_weight = prior_weight;
@@ -1026,17 +1028,35 @@ int tpe_plan_num_levels(tpe_plan_t p, int32_t *n) {
 int tpe_plan_set_history(tpe_plan_t p, const double *losses, const double *vals,
                          const uint8_t *active, int64_t n, int32_t on_device, void *stream) {
   if (!p) return TPE_E_INVALID;
+  return tpe_plan_update_history(p, n, 0, n, vals, active, n, 0, losses, on_device, stream);
+}
+
+// Rows live at stride ncap (FitArgs::ld), so appending trials leaves the rows
+// already on the device in place: a call copies only the rows it is given.
+int tpe_plan_update_history(tpe_plan_t p, int64_t n, int64_t row0, int64_t n_rows,
+                            const double *vals, const uint8_t *active, int64_t src_ld,
+                            int64_t loss0, const double *losses, int32_t on_device,
+                            void *stream) {
+  if (!p) return TPE_E_INVALID;
   tpe_engine *h = p->eng;
   if (n < 0 || n > p->ncap) return fail(h, TPE_E_INVALID, "history larger than max_trials");
-  if (n > 0 && (!losses || !vals || !active)) return fail(h, TPE_E_INVALID, "bad args");
+  if (row0 < 0 || n_rows < 0 || row0 + n_rows > n || loss0 < 0 || loss0 > n)
+    return fail(h, TPE_E_INVALID, "history rows out of range");
+  if (n_rows > 0 && (!vals || !active || src_ld < n_rows))
+    return fail(h, TPE_E_INVALID, "bad history rows");
+  if (loss0 < n && !losses) return fail(h, TPE_E_INVALID, "losses missing");
   CKH(hipSetDevice(h->device));
   hipStream_t st = pick_stream(h, stream);
   const hipMemcpyKind kd = on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+  if (n_rows > 0 && p->P > 0) {
+    CKH(hipMemcpy2DAsync(p->d_vals + row0, (size_t)p->ncap * 8, vals, (size_t)src_ld * 8,
+                         (size_t)n_rows * 8, (size_t)p->P, kd, st));
+    CKH(hipMemcpy2DAsync(p->d_active + row0, (size_t)p->ncap, active, (size_t)src_ld,
+                         (size_t)n_rows, (size_t)p->P, kd, st));
+  }
+  if (loss0 < n)
+    CKH(hipMemcpyAsync(p->d_losses + loss0, losses, (size_t)(n - loss0) * 8, kd, st));
   p->n = n;
-  if (n == 0) return TPE_OK;
-  CKH(hipMemcpyAsync(p->d_losses, losses, n * 8, kd, st));
-  CKH(hipMemcpyAsync(p->d_vals, vals, (size_t)n * p->P * 8, kd, st));
-  CKH(hipMemcpyAsync(p->d_active, active, (size_t)n * p->P, kd, st));
   if (!on_device) CKH(hipStreamSynchronize(st));
   return TPE_OK;
 }
@@ -1218,6 +1238,7 @@ int tpe_plan_fit_suggest(tpe_plan_t p, double gamma, int32_t gamma_cap, double p
   key.n_cand = n_cand;
   key.stream = (void *)st;
   key.table = (int64_t)nb + 1 <= kTabCap;
+  key.fuse = (int64_t)nb + 1 <= kFuseTab;
   int rc = ensure_suggest_state(h, p, n_sug, 1);
   if (rc) return rc;
   p->h_seeds.assign(seeds, seeds + n_sug);

@@ -875,8 +875,8 @@ __global__ __launch_bounds__(kFitThreads) void k_fit(FitArgs A) {
   // ---- gather this side's observations in tid order (tpe.py:629-636):
   // 4 consecutive trials per thread, one block scan per 4096 trials
   const bool cat = H.family == TPE_CAT;
-  const double *row = A.vals + (int64_t)hp * A.n;
-  const uint8_t *arow = A.active + (int64_t)hp * A.n;
+  const double *row = A.vals + (int64_t)hp * A.ld;
+  const uint8_t *arow = A.active + (int64_t)hp * A.ld;
   double *ob = A.ob + slot * A.kcap;
   uint64_t *lk = reinterpret_cast<uint64_t *>(dyn_lds + kOffKeys);
   int m = 0, nlt = 0;

@@ -139,10 +139,11 @@ struct ScoreArgs {
 // Arguments of the fit kernels (tpe_fit.hip), one block per (hp, side) slot.
 struct FitArgs {
   const tpe_hp *hps;
-  const double *vals;        // [P][n] history values (tid order)
-  const uint8_t *active;     // [P][n]
+  const double *vals;        // [P][ld] history values (tid order)
+  const uint8_t *active;     // [P][ld]
   const double *losses;      // [n]
   int64_t n;
+  int64_t ld;                // row stride of vals / active (the plan's trial capacity)
   int32_t n_below;
   int32_t lf;
   double prior_weight;

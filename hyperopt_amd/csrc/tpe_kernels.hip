@@ -30,13 +30,6 @@ constexpr int kSortMax = 8192;  // candidates per bucketing chunk
 // the per-draw rejection sampler runs (!TAB), in a kernel of its own so the
 // table path keeps its small register footprint.
 constexpr int kDrawThreads = 256;
-__device__ __attribute__((noinline)) double draw_one_ool(const tpe_hp *Hp, const MixInfo *I,
-                                                       const double *w, const double *mu,
-                                                       const double *sg, uint64_t seed,
-                                                       uint64_t gi, uint32_t stream) {
-  return draw_one(*Hp, *I, w, mu, sg, seed, gi, stream);
-}
-
 template <bool TAB>
 __global__ __launch_bounds__(kDrawThreads) void k_draw(ScoreArgs A) {
   if constexpr (TAB) {

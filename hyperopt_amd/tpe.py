@@ -5,13 +5,19 @@ Same call as the reference (hyperopt/tpe.py:804-897)::
     suggest(new_ids, domain, trials, seed, prior_weight=1.0, n_startup_jobs=20,
             n_EI_candidates=24, gamma=0.25, linear_forgetting=25)
 
-Host side (this module): history assembly -- dedupe by tid / from_tid, loss
-None -> +inf, tid order (tpe.py:820-848) -- into columns, the startup
-fallback to ``rand.suggest``, and the write-back of the winning values
-(tpe.py:887-897).  Device side (libtpe_engine.so, one plan per Domain): the
-good/bad split, every hyperparameter's two Parzen fits, candidate draws,
-below/above lpdf and the EI argmax, level by level through conditional
-choices.  There is no CPU fallback: without the engine this raises.
+Host side (this module): the trial history is a columnar mirror of the
+Trials (``history.TrialHistory``: tpe.py:820-848 semantics, synced
+incrementally and copied to the device row by row), the startup fallback to
+``rand.suggest`` and the write-back of the winning values (tpe.py:887-897).
+Device side (libtpe_engine.so, one plan per Domain): the good/bad split,
+every hyperparameter's two Parzen fits, candidate draws, below/above lpdf
+and the EI argmax, level by level through conditional choices.  There is no
+CPU fallback: without the engine this raises.
+
+``new_ids`` may hold several ids (the reference accepts exactly one,
+tpe.py:812): the suggestions are served by ONE batched engine call on the
+same history, suggestion s drawing its candidates with ``batch_seeds(seed,
+S)[s]`` (s = 0 uses ``seed`` itself, so a single suggestion is unchanged).
 
 ``rng_stream='numpy'`` replays the reference's RandomState candidate stream
 (hyperopt draws in its interpreter order): the fit and the scoring stay on the
@@ -25,12 +31,14 @@ from __future__ import annotations
 import logging
 import math
 import threading
+import weakref
 
 import numpy as np
 
 from . import _engine as E
 from . import rand, rstream
 from .base import miscs_update_idxs_vals
+from .history import TrialHistory
 
 logger = logging.getLogger(__name__)
 
@@ -44,62 +52,78 @@ _default_n_startup_jobs = 20
 _default_linear_forgetting = DEFAULT_LF
 
 
-# --------------------------------------------------------------------------
-# history assembly (tpe.py:820-848 + base.miscs_to_idxs_vals)
-# --------------------------------------------------------------------------
-def build_history(domain, trials, labels):
-    """Return (tids, losses[N], vals[P,N], active[P,N]) in tid order."""
-    best_loss, best_doc = {}, {}
-    for doc in trials.trials:
-        tid = doc['misc'].get('from_tid', doc['tid'])
-        loss = domain.loss(doc['result'], doc['spec'])
-        loss = float('inf') if loss is None else float(loss)
-        best_loss.setdefault(tid, loss)
-        if loss <= best_loss[tid]:
-            best_loss[tid] = loss
-            best_doc[tid] = doc
-    tids = sorted(best_doc)
-    n, p = len(tids), len(labels)
-    losses = np.fromiter((best_loss[t] for t in tids), dtype=np.float64, count=n)
-    vals = np.zeros((p, n))
-    active = np.zeros((p, n), dtype=np.uint8)
-    for j, t in enumerate(tids):
-        misc = best_doc[t]['misc']
-        mi, mv = misc['idxs'], misc['vals']
-        for i, lab in enumerate(labels):
-            ix = mi[lab]
-            # the reference matches observations by misc tid against the
-            # (from_tid-aware) loss tids (tpe.py:629-636)
-            if ix and ix[0] == t:
-                vals[i, j] = float(mv[lab][0])
-                active[i, j] = 1
-    return tids, losses, vals, active
+def build_history(domain, trials, labels=None):
+    """(tids, losses[N], vals[P, N], active[P, N]) of ``trials`` in tid
+    order -- the reference's history assembly (tpe.py:820-848), from a
+    fresh columnar mirror.  ``labels`` must be the domain's (sorted) labels."""
+    h = TrialHistory(domain)
+    if labels is not None and list(labels) != h.labels:
+        raise ValueError('labels must be the domain space labels')
+    return h.sync(trials).columns()
+
+
+def batch_seeds(seed, n):
+    """Per-suggestion Philox keys of a batch: ``seed`` first, then splitmix64
+    steps of it (independent streams; deterministic in (seed, position))."""
+    out = [int(seed) & (2 ** 64 - 1)]
+    z = out[0]
+    for _ in range(1, n):
+        z = (z + 0x9E3779B97F4A7C15) & (2 ** 64 - 1)
+        x = z
+        x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & (2 ** 64 - 1)
+        x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & (2 ** 64 - 1)
+        out.append(x ^ (x >> 31))
+    return out
 
 
 # --------------------------------------------------------------------------
-# per-Domain device state
+# per-Domain device state: the plan, and one history mirror per Trials
 # --------------------------------------------------------------------------
 class _State(object):
     def __init__(self):
         self.plan = None
-        self.cap = 0
         self.lock = threading.Lock()
+        self.histories = weakref.WeakKeyDictionary()
+
+    def history(self, domain, trials):
+        h = self.histories.get(trials)
+        if h is None:
+            h = self.histories[trials] = TrialHistory(domain)
+        return h
+
+    def plan_for(self, domain, n, engine):
+        p = self.plan
+        if p is None or p.max_trials < n or p.engine is not engine:
+            cap = max(64, 1 << max(0, int(math.ceil(math.log2(max(n, 1))))))
+            hps, conds, pprior = domain.space.engine_tables()
+            self.plan = p = E.Plan(engine, hps, conds, pprior, cap)
+        return p
 
 
-def _domain_plan(domain, n_trials, engine):
+def _state(domain):
     st = domain.__dict__.get('_tpe_state')
     if st is None:
         st = domain.__dict__.setdefault('_tpe_state', _State())
-    if st.plan is None or st.cap < n_trials or st.plan.engine is not engine:
-        cap = max(64, 1 << max(0, int(math.ceil(math.log2(max(n_trials, 1))))))
-        hps, conds, pprior = domain.space.engine_tables()
-        st.plan = E.Plan(engine, hps, conds, pprior, cap)
-        st.cap = cap
+    return st
+
+
+def _domain_plan(domain, n_trials, engine):
+    """The domain's plan, sized for ``n_trials`` (tools / tests)."""
+    st = _state(domain)
+    st.plan_for(domain, n_trials, engine)
     return st
 
 
 def _fmt(h, v):
     return int(round(v)) if h.is_categorical else float(v)
+
+
+def _new_doc(domain, trials, cs, new_id, chosen):
+    idxs = {lab: ([new_id] if lab in chosen else []) for lab in cs.labels}
+    vls = {lab: ([chosen[lab]] if lab in chosen else []) for lab in cs.labels}
+    misc = dict(tid=new_id, cmd=domain.cmd, workdir=domain.workdir)
+    miscs_update_idxs_vals([misc], idxs, vls)
+    return trials.new_trial_docs([new_id], [None], [domain.new_result()], [misc])[0]
 
 
 def suggest(new_ids, domain, trials, seed,
@@ -109,37 +133,41 @@ def suggest(new_ids, domain, trials, seed,
             gamma=_default_gamma,
             linear_forgetting=_default_linear_forgetting,
             rng_stream='philox', engine=None):
-    """hyperopt/tpe.py:804-897 on the GPU.  ``linear_forgetting`` is accepted
-    and, as in the reference (tpe.py:809), not used: LF is fixed at 25."""
-    new_id, = new_ids
+    """hyperopt/tpe.py:804-897 on the GPU, one document per id in
+    ``new_ids``.  ``linear_forgetting`` is accepted and, as in the reference
+    (tpe.py:809), not used: LF is fixed at 25."""
+    new_ids = list(new_ids)
+    if not new_ids:
+        return []
+    if rng_stream not in ('philox', 'numpy'):
+        raise ValueError('rng_stream must be "philox" or "numpy"')
     cs = domain.space
-    tids, losses, vals, active = build_history(domain, trials, cs.labels)
-    if len(tids) < n_startup_jobs:
-        return rand.suggest(new_ids, domain, trials, seed)
-    engine = engine or E.default_engine()
-    st = _domain_plan(domain, len(tids), engine)
+    st = _state(domain)
     with st.lock:
-        plan = st.plan
-        plan.set_history(losses, vals, active)
+        hist = st.history(domain, trials).sync(trials)
+        if hist.n < n_startup_jobs:
+            return rand.suggest(new_ids, domain, trials, seed)
+        engine = engine or E.default_engine()
+        plan = st.plan_for(domain, hist.n, engine)
+        hist.push(plan)
+        seeds = batch_seeds(seed, len(new_ids))
+        n_ei = int(n_EI_candidates)
         if rng_stream == 'philox':
-            # fit + sample + score + argmax in one engine call (graph replay)
-            res = plan.fit_suggest([int(seed)], int(n_EI_candidates), gamma=gamma,
-                                   prior_weight=prior_weight, lf=DEFAULT_LF)[0]
-            chosen = {}
-            for h in cs.hps:
-                r = res[h.index]
-                if r['active'] and r['index'] >= 0:
-                    chosen[h.label] = _fmt(h, r['value'])
-        elif rng_stream == 'numpy':
-            plan.fit(gamma=gamma, prior_weight=prior_weight, lf=DEFAULT_LF)
-            chosen = _suggest_numpy_stream(cs, plan, seed, int(n_EI_candidates))
+            # fit + sample + score + argmax of every suggestion in one call
+            res = plan.fit_suggest(seeds, n_ei, gamma=gamma, prior_weight=prior_weight,
+                                   lf=DEFAULT_LF)
+            picks = []
+            for s in range(len(new_ids)):
+                chosen = {}
+                for h in cs.hps:
+                    r = res[s, h.index]
+                    if r['active'] and r['index'] >= 0:
+                        chosen[h.label] = _fmt(h, r['value'])
+                picks.append(chosen)
         else:
-            raise ValueError('rng_stream must be "philox" or "numpy"')
-    idxs = {lab: ([new_id] if lab in chosen else []) for lab in cs.labels}
-    vls = {lab: ([chosen[lab]] if lab in chosen else []) for lab in cs.labels}
-    misc = dict(tid=new_id, cmd=domain.cmd, workdir=domain.workdir)
-    miscs_update_idxs_vals([misc], idxs, vls)
-    return trials.new_trial_docs([new_id], [None], [domain.new_result()], [misc])
+            plan.fit(gamma=gamma, prior_weight=prior_weight, lf=DEFAULT_LF)
+            picks = [_suggest_numpy_stream(cs, plan, sd, n_ei) for sd in seeds]
+    return [_new_doc(domain, trials, cs, i, c) for i, c in zip(new_ids, picks)]
 
 
 def _suggest_numpy_stream(cs, plan, seed, n_ei):

@@ -155,6 +155,18 @@ int tpe_plan_set_history(tpe_plan_t p, const double *losses,
                          const double *vals, const uint8_t *active, int64_t n,
                          int32_t on_device, void *stream);
 
+/* Incremental history update (the columnar trial store appends rows): copy
+ * rows [row0, row0 + n_rows) of every hp from vals / active (source layout
+ * [n_hp][src_ld]: row r of hp i at vals[i * src_ld + (r - row0)]) and
+ * losses [loss0, n) from losses[0 .. n - loss0); the history length becomes
+ * n.  Rows outside [row0, row0 + n_rows) keep their device contents.
+ * tpe_plan_set_history(n) == update_history(n, 0, n, vals, active, n, 0,
+ * losses).  Replaces the per-call re-walk of hyperopt/tpe.py:820-848.      */
+int tpe_plan_update_history(tpe_plan_t p, int64_t n, int64_t row0, int64_t n_rows,
+                            const double *vals, const uint8_t *active, int64_t src_ld,
+                            int64_t loss0, const double *losses, int32_t on_device,
+                            void *stream);
+
 /* split + Parzen fit of every hp, both sides (tpe.py:613-641, 398-607).    */
 int tpe_plan_fit(tpe_plan_t p, double gamma, int32_t gamma_cap,
                  double prior_weight, int32_t lf, void *stream);

@@ -335,3 +335,74 @@ def test_graph_replay_in_child_process():
     r = subprocess.run([sys.executable, '-c', code], cwd=root, env=dict(os.environ, TPE_GRAPH='1'),
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and 'OK' in r.stdout, (r.stdout[-1000:], r.stderr[-3000:])
+
+
+def test_batched_suggest_equals_single_seed_suggests():
+    """Config 5's path: one batched fit_suggest over S seeds equals S
+    single-seed calls bit for bit (suggestion s reads only its own seed), on
+    a conditional and a mixed space, for S beyond the 8 inline seeds."""
+    for name in ('cfg2', 'cond'):
+        meta, d, dom, trials = _fixture_trials(name)
+        tpe.suggest([meta['new_id']], dom, trials, 7, n_EI_candidates=64)
+        plan = dom._tpe_state.plan
+        seeds = tpe.batch_seeds(1234, 11)
+        for n in (300, 4096):
+            got = plan.fit_suggest(seeds, n)
+            for s, sd in enumerate(seeds):
+                one = plan.fit_suggest([sd], n)[0]
+                np.testing.assert_array_equal(got[s].view(np.uint8), one.view(np.uint8),
+                                              err_msg='%s s=%d n=%d' % (name, s, n))
+
+
+def test_tpe_suggest_batch_of_ids_matches_single_calls():
+    """tpe.suggest with several new ids = one engine call; each returned doc
+    equals the single-id suggest with that suggestion's batch seed."""
+    meta, d, dom, trials = _fixture_trials('cond')
+    ids = [meta['new_id'] + i for i in range(5)]
+    docs = tpe.suggest(ids, dom, trials, 99, n_EI_candidates=512)
+    assert [x['tid'] for x in docs] == ids
+    for i, sd in enumerate(tpe.batch_seeds(99, 5)):
+        one = tpe.suggest([ids[i]], dom, trials, sd, n_EI_candidates=512)[0]
+        assert docs[i]['misc']['vals'] == one['misc']['vals'], i
+
+
+def test_incremental_device_history_equals_fresh_upload():
+    """An fmin run grows the device history row by row (columnar store +
+    tpe_plan_update_history); a fresh plan loaded from scratch with the final
+    trials must give the same suggestion bit for bit."""
+    t = Trials()
+    algo = functools.partial(tpe.suggest, n_EI_candidates=256, n_startup_jobs=10)
+    space = spaces.cond_space(hp)
+    fmin(lambda x: float(np.sin(3 * x['aa'])), space, algo=algo, max_evals=60, trials=t,
+         rstate=np.random.RandomState(3))
+    dom = Domain(lambda x: 0.0, space)
+    a = tpe.suggest([1000], dom, t, 5, n_EI_candidates=256, n_startup_jobs=10)[0]
+    hist = dom._tpe_state.histories[t]
+    assert hist.n == 60
+    for k in range(3):     # incremental steps on the same plan
+        (nid,) = t.new_trial_ids(1)
+        t.insert_trial_docs(tpe.suggest([nid], dom, t, 11 + k, n_EI_candidates=256,
+                                        n_startup_jobs=10))
+        t.refresh()
+        t.trials[-1]['result'] = {'status': 'ok', 'loss': float(k) - 5.0}
+        t.trials[-1]['state'] = H.JOB_STATE_DONE
+    inc = tpe.suggest([2000], dom, t, 5, n_EI_candidates=256, n_startup_jobs=10)[0]
+    fresh_dom = Domain(lambda x: 0.0, space)
+    ref = tpe.suggest([2000], fresh_dom, t, 5, n_EI_candidates=256, n_startup_jobs=10)[0]
+    assert inc['misc']['vals'] == ref['misc']['vals']
+    assert a['misc']['vals'] != {} and dom._tpe_state.histories[t].n == 63
+
+
+def test_thread_trials_async_batched_tpe():
+    """Asynchronous workers + batched TPE suggestions (max_queue_len > 1):
+    completes, every trial evaluated once, reaches the quadratic's optimum."""
+    t = H.ThreadTrials(n_workers=4)
+    try:
+        fmin(lambda x: (x - 3) ** 2, hp.uniform('x', -5, 5),
+             algo=functools.partial(tpe.suggest, n_EI_candidates=1024), max_evals=120,
+             trials=t, rstate=np.random.RandomState(1), max_queue_len=4)
+    finally:
+        t.shutdown()
+    assert len(t) == 120
+    assert all(d['state'] == H.JOB_STATE_DONE for d in t.trials)
+    assert min(t.losses()) < 1e-2
