@@ -154,6 +154,13 @@ def load_library(path: str = LIB_PATH):
         return lib
 
 
+def _seeds(seeds):
+    """uint64 seed array (exact: a mixed list of Python ints would round
+    through float64 in np.asarray)."""
+    seeds = [int(x) & (2 ** 64 - 1) for x in np.atleast_1d(np.asarray(seeds, dtype=object))]
+    return np.fromiter(seeds, dtype=np.uint64, count=len(seeds))
+
+
 def _dp(a):
     return None if a is None else a.ctypes.data_as(_D)
 
@@ -401,7 +408,7 @@ class Plan(object):
         unless ``out`` is a device pointer (int) or ``fetch`` is False (the
         results stay in the plan: ``results_device_ptr()`` / ``results()``)."""
         e = self.engine
-        seeds = np.ascontiguousarray(np.atleast_1d(seeds), dtype=np.uint64)
+        seeds = _seeds(seeds)
         host = out is None and fetch
         res = np.empty((seeds.size, self.n_hp), dtype=RESULT_DTYPE) if host else None
         optr = res.ctypes.data if host else out
@@ -417,7 +424,7 @@ class Plan(object):
         """fit() + suggest() over all levels in one engine call; repeated calls
         of one shape replay a captured hipGraph of the step (tpe_engine.h)."""
         e = self.engine
-        seeds = np.ascontiguousarray(np.atleast_1d(seeds), dtype=np.uint64)
+        seeds = _seeds(seeds)
         host = out is None and fetch
         res = np.empty((seeds.size, self.n_hp), dtype=RESULT_DTYPE) if host else None
         optr = res.ctypes.data if host else out

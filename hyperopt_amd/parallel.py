@@ -126,7 +126,7 @@ class ShardedSuggest(object):
 
     def suggest(self, seeds, n_cand, fetch=True):
         import torch
-        seeds = np.ascontiguousarray(np.atleast_1d(seeds), dtype=np.uint64)
+        seeds = E._seeds(seeds)
         S, P = seeds.size, self.plan.n_hp
         begin, count = shard_range(int(n_cand), self.rank, self.world)
         stream = self.stream.cuda_stream

@@ -245,16 +245,21 @@ class Trials(object):
         st = self._store
         mask = self._visible_mask(st.state.view(), st.keys)
         old = self._mask
-        if old.size and not np.array_equal(mask[:old.size], old):
-            self._epoch += 1      # not a pure extension: consumers rebuild
-        # the visible tids join the known ids; only newly visible documents
-        # can add any (the set is never shrunk, as in the reference)
-        fresh = mask.copy()
         n_old = min(old.size, mask.size)
-        fresh[:n_old] &= ~old[:n_old]
-        st.ids.update(d['tid'] for d in itertools.compress(st.docs, fresh))
+        if old.size <= mask.size and np.array_equal(mask[:n_old], old):
+            # a pure extension (the common case): only the new documents
+            # are looked at; the list is a new object as in the reference
+            add = list(itertools.compress(st.docs[n_old:], mask[n_old:]))
+            st.ids.update(d['tid'] for d in add)
+            self._trials = self._trials + add
+        else:
+            self._epoch += 1      # an earlier document dropped out: consumers rebuild
+            # the visible tids join the known ids (the set never shrinks)
+            fresh = mask.copy()
+            fresh[:n_old] &= ~old[:n_old]
+            st.ids.update(d['tid'] for d in itertools.compress(st.docs, fresh))
+            self._trials = list(itertools.compress(st.docs, mask))
         self._mask = mask
-        self._trials = list(itertools.compress(st.docs, mask))
 
     @property
     def trials(self):
@@ -377,6 +382,7 @@ class Trials(object):
         self.attachments = {}
         self._epoch += 1
         self._mask = np.zeros(0, dtype=bool)
+        self._trials = []
         self.refresh()
 
     # -- state counts (base.py:481-509), on the state column -----------------

@@ -346,6 +346,76 @@ def gen_suggest():
         json.dump(meta, f, indent=1)
 
 
+# ---------------------------------------------------------------- configs 3 / 4 at size
+def _keep(per, order, picks):
+    """The captured calls of the labels in ``picks`` (capture order is the
+    reference interpreter's hp order ``order``)."""
+    out = []
+    for lab in picks:
+        k = order.index(lab)
+        out.append((lab, per[k]))
+    return out
+
+
+def gen_big():
+    """Config 4 (100 x uniform(-5, 5), N = 1e4: K_a ~ 9976) and config 3 (50-hp
+    conditional, N = 1e4) at full history size with 4096 reference-drawn
+    candidates per hp; only a few hps' candidates / lliks are stored."""
+    meta = {}
+    # -- config 4: SURVEY 8(d) history, obs RandomState(1), losses RandomState(2)
+    n, D = 10000, 100
+    U = np.random.RandomState(1).uniform(-5, 5, (n, D))
+    L = np.random.RandomState(2).rand(n)
+    domain = base.Domain(lambda x: 0.0, spaces.cfg4_space(hp, D))
+    labels = ['x%d' % i for i in range(D)]
+    t = Trials()
+    miscs = [dict(tid=j, cmd=domain.cmd, workdir=None,
+                  idxs={lab: [j] for lab in labels},
+                  vals={lab: [float(U[j, i])] for i, lab in enumerate(labels)})
+             for j in range(n)]
+    docs = t.new_trial_docs(list(range(n)), [None] * n,
+                            [{'status': base.STATUS_OK, 'loss': float(l)} for l in L], miscs)
+    for d in docs:
+        d['state'] = base.JOB_STATE_DONE
+    t.insert_trial_docs(docs)
+    t.refresh()
+    docs, per = capture_suggest(domain, t, 7, n_EI_candidates=4096)
+    order = sorted(labels, reverse=True)          # the interpreter's hp order here
+    assert len(per) == D
+    picks = ['x0', 'x7', 'x42', 'x99']
+    kept = _keep(per, order, picks)
+    d = {}
+    pack(d, 'samples', [p['samples'] for _, p in kept])
+    pack(d, 'llik_b', [p['llik_b'] for _, p in kept])
+    pack(d, 'llik_a', [p['llik_a'] for _, p in kept])
+    out_vals = docs[0]['misc']['vals']
+    d['chosen'] = np.array([float(out_vals[lab][0]) for lab in picks])
+    np.savez_compressed(os.path.join(HERE, 'suggest_cfg4.npz'), **d)
+    meta['cfg4'] = dict(labels=picks, n=n, D=D, obs_seed=1, loss_seed=2, suggest_seed=7,
+                        kw=dict(n_EI_candidates=4096), new_id=n)
+    print('cfg4 kept', picks, d['chosen'])
+    # -- config 3: rand.suggest history seed 1, losses RandomState(2)
+    domain = base.Domain(lambda x: 0.0, spaces.cfg3_space(hp))
+    trials = history_from_rand(domain, 10000, 1, 2)
+    docs, per = capture_suggest(domain, trials, 7, n_EI_candidates=4096)
+    sizes = [p['samples'].size for p in per]
+    live = [k for k, z in enumerate(sizes) if z > 0]
+    d = {}
+    pack(d, 'samples', [per[k]['samples'] for k in live])
+    pack(d, 'llik_b', [per[k]['llik_b'] for k in live])
+    pack(d, 'llik_a', [per[k]['llik_a'] for k in live])
+    labs = sorted(domain.params.keys())
+    out_vals = docs[0]['misc']['vals']
+    d['chosen'] = np.array([float(out_vals[lab][0]) if out_vals[lab] else np.nan for lab in labs])
+    d['call_index'] = np.array(live, dtype=np.int64)
+    np.savez_compressed(os.path.join(HERE, 'suggest_cfg3_full.npz'), **d)
+    meta['cfg3_full'] = dict(labels=labs, n=10000, hist_seed=1, loss_seed=2, suggest_seed=7,
+                             kw=dict(n_EI_candidates=4096), new_id=10000, n_calls=len(per))
+    print('cfg3 full: calls', len(per), 'with candidates', live)
+    with open(os.path.join(HERE, 'suggest_big_meta.json'), 'w') as f:
+        json.dump(meta, f, indent=1)
+
+
 # ---------------------------------------------------------------- TestOpt runs
 def gen_testopt():
     """fmin trajectories of the reference's TestOpt (test_tpe.py:517-641)."""
@@ -375,7 +445,8 @@ def gen_testopt():
 if __name__ == '__main__':
     np.seterr(all='ignore')
     gens = dict(split=gen_split, parzen=gen_parzen, lpdf=gen_lpdf, categorical=gen_categorical,
-                samplers=gen_samplers, cfg1=gen_cfg1, suggest=gen_suggest, testopt=gen_testopt)
+                samplers=gen_samplers, cfg1=gen_cfg1, suggest=gen_suggest, testopt=gen_testopt,
+                big=gen_big)
     for name, g in gens.items():
         if not ONLY or name in ONLY:
             g()

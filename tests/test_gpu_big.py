@@ -1,0 +1,173 @@
+"""Parity at BASELINE sizes (configs 3, 4, 5) on the GPU.
+
+* config 4 (K_a ~ 9976): the reference's own 4096 candidates per hp scored
+  by the plan against the reference lliks (suggest_cfg4.npz), and a full
+  1e7-candidate suggest whose argmax equals the device merge of two shards;
+* config 3 (N = 1e4 conditional): the reference's candidates of the winning
+  branch scored against its lliks (suggest_cfg3_full.npz);
+* config 5 (batched suggestions): every suggestion of a batch equals the
+  oracle's argmax over that suggestion's own candidates.
+The max |delta lpdf| seen is written to $TPE_PARITY_REPORT (JSON) if set.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from hyperopt_amd import hp, tpe, rand, Trials, _engine as E
+from hyperopt_amd.base import Domain
+
+from golden_io import load, load_json, unpack
+from gpu_util import assert_close, argmax_equiv
+import big_configs
+import spaces
+
+pytestmark = pytest.mark.gpu
+_REPORT = {}
+
+
+def _record(key, got, want):
+    got, want = np.asarray(got), np.asarray(want)
+    fin = np.isfinite(got) & np.isfinite(want)
+    d = np.abs(got[fin] - want[fin])
+    rel = d / np.maximum(1.0, np.abs(want[fin]))
+    _REPORT[key] = dict(max_abs=float(d.max()) if d.size else 0.0,
+                        max_rel=float(rel.max()) if rel.size else 0.0, n=int(fin.sum()))
+    path = os.environ.get('TPE_PARITY_REPORT')
+    if path:
+        with open(path, 'w') as f:
+            json.dump(_REPORT, f, indent=1, sort_keys=True)
+
+
+@pytest.fixture(scope='module')
+def cfg4_plan():
+    dom, L, vals, act = big_configs.cfg4_domain_history(hp, Domain)
+    hps, conds, pprior = dom.space.engine_tables()
+    plan = E.Plan(E.default_engine(), hps, conds, pprior, max_trials=L.size)
+    plan.set_history(L, vals, act)
+    plan.fit()
+    return dom, plan
+
+
+def test_config4_reference_candidates(cfg4_plan):
+    dom, plan = cfg4_plan
+    meta = load_json('suggest_big_meta.json')['cfg4']
+    d = load('suggest_cfg4.npz')
+    for k, lab in enumerate(meta['labels']):
+        h = dom.space.by_label[lab]
+        assert plan.mixture(h.index, 1)[0].size >= 9900          # K_a ~ 9976
+        x = unpack(d, 'samples', k)
+        lb, la, bi, bs = plan.score_candidates(h.index, x)
+        rb, ra = unpack(d, 'llik_b', k), unpack(d, 'llik_a', k)
+        assert_close(lb, rb, msg='cfg4 %s below' % lab)
+        assert_close(la, ra, msg='cfg4 %s above' % lab)
+        _record('cfg4_%s_below' % lab, lb, rb)
+        _record('cfg4_%s_above' % lab, la, ra)
+        assert argmax_equiv(rb - ra, bi), lab
+        assert x[bi] == d['chosen'][k] or argmax_equiv(rb - ra, bi)
+
+
+def test_config4_full_draw_shard_merge(cfg4_plan):
+    """1e7 candidates per hp (the config-4 workload): one device equals the
+    k_merge of two candidate shards, index and value, for all 100 hps."""
+    torch = pytest.importorskip('torch')
+    dom, plan = cfg4_plan
+    n, cut = 10_000_000, 4_321_987
+    full = plan.suggest([7], n)
+    parts = [plan.suggest([7], cut, cand_begin=0), plan.suggest([7], n - cut, cand_begin=cut)]
+    raw = torch.from_numpy(np.stack(parts).view(np.uint8).reshape(-1).copy()).cuda()
+    merged = plan.merge(raw.data_ptr(), world=2, level=0)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(merged['index'], full['index'])
+    np.testing.assert_array_equal(merged['value'], full['value'])
+    assert (full['index'] >= 0).all() and (full['index'] < n).all()
+    assert np.all((full['value'] >= -5) & (full['value'] < 5))
+
+
+def test_config3_reference_candidates_full_history():
+    from oracle import tpe_oracle as O
+    from oracle_algo import oracle_hps
+    meta = load_json('suggest_big_meta.json')['cfg3_full']
+    d = load('suggest_cfg3_full.npz')
+    dom, t = big_configs.cfg3_trials(hp, Domain, Trials, rand, meta['n'])
+    tpe.suggest([meta['new_id']], dom, t, 7, n_EI_candidates=64)
+    plan = dom._tpe_state.plan
+    cs = dom.space
+    tids, losses, vals, active = tpe.build_history(dom, t, cs.labels)
+    tids = np.asarray(tids)
+    ohps = oracle_hps(cs)
+    for j, k in enumerate(d['call_index']):
+        lab = cs.draw_order[k]
+        h = cs.by_label[lab]
+        x = unpack(d, 'samples', j)
+        lb, la, bi, bs = plan.score_candidates(h.index, x)
+        i = h.index
+        ot, ov = tids[active[i] == 1], vals[i][active[i] == 1]
+        bo, ao = O.split_observations(ot, ov, tids, losses, 0.25, kind='stable')
+        with np.errstate(all='ignore'):
+            r = O.score_hp(ohps[lab]['dist'], ohps[lab]['args'], bo, ao, 1.0, x, kind='stable')
+            ru = O.score_hp(ohps[lab]['dist'], ohps[lab]['args'], bo, ao, 1.0, x, kind=None)
+        assert_close(lb, r['llik_b'], msg='cfg3 %s below vs oracle' % lab)
+        assert_close(la, r['llik_a'], msg='cfg3 %s above vs oracle' % lab)
+        rb, ra = unpack(d, 'llik_b', j), unpack(d, 'llik_a', j)
+        if np.array_equal(ru['llik_a'], r['llik_a'], equal_nan=True) and \
+                np.array_equal(ru['llik_b'], r['llik_b'], equal_nan=True):
+            assert_close(lb, rb, msg='cfg3 %s below' % lab)
+            assert_close(la, ra, msg='cfg3 %s above' % lab)
+            _record('cfg3_%s_below' % lab, lb, rb)
+            _record('cfg3_%s_above' % lab, la, ra)
+        with np.errstate(all='ignore'):
+            assert argmax_equiv(r['llik_b'] - r['llik_a'], bi), lab
+
+
+def test_config5_batched_suggestions_equal_oracle_argmax():
+    """Config 5's path (batched suggestions on config 2's space and history):
+    for each suggestion s, regenerate its candidates of every hp on the host
+    side of the ABI (tpe_sample: the same counter-based draws, key = the
+    suggestion's seed, stream = hp), score them with the oracle, and require
+    the batch's winner to be the oracle's argmax (1e-6 EI ties allowed)."""
+    from oracle import tpe_oracle as O
+    from oracle_algo import oracle_hps
+    meta = load_json('suggest_meta.json')['cfg2']
+    dcfg = load('suggest_cfg2.npz')
+    dom = Domain(lambda x: 0.0, spaces.cfg2_space(hp))
+    docs = rand.suggest(list(range(meta['n'])), dom, Trials(), meta['hist_seed'])
+    for doc, l in zip(docs, dcfg['losses']):
+        doc['state'] = 2
+        doc['result'] = {'status': 'ok', 'loss': float(l)}
+    from hyperopt_amd import trials_from_docs
+    t = trials_from_docs(docs)
+    tpe.suggest([meta['new_id']], dom, t, 7, n_EI_candidates=64)
+    plan = dom._tpe_state.plan
+    eng = plan.engine
+    seeds = tpe.batch_seeds(2024, 16)
+    n = 4096
+    res = plan.fit_suggest(seeds, n)
+    cs = dom.space
+    tids, losses, vals, active = tpe.build_history(dom, t, cs.labels)
+    tids = np.asarray(tids)
+    ohps = oracle_hps(cs)
+    tabs = cs.engine_tables()[0]
+    for h in cs.hps:
+        i = h.index
+        ot, ov = tids[active[i] == 1], vals[i][active[i] == 1]
+        bo, ao = O.split_observations(ot, ov, tids, losses, 0.25, kind='stable')
+        w, mu, sg = plan.mixture(i, 0)
+        tb = tabs[i]
+        lo = tb.low if tb.flags & E.HAS_LOW else None
+        hi = tb.high if tb.flags & E.HAS_HIGH else None
+        q = tb.q if tb.flags & E.HAS_Q else None
+        for s, sd in enumerate(seeds):
+            if tb.family == E.CAT:
+                x = eng.sample(E.CAT, w, seed=sd, stream=i, n=n)
+            else:
+                x = eng.sample(tb.family, w, mu, sg, lo, hi, q, seed=sd, stream=i, n=n)
+            with np.errstate(all='ignore'):
+                r = O.score_hp(ohps[h.label]['dist'], ohps[h.label]['args'], bo, ao, 1.0, x,
+                               kind='stable')
+                sc = r['llik_b'] - r['llik_a']
+            got = res[s, i]
+            assert got['active'] == 1 and 0 <= got['index'] < n, (h.label, s)
+            assert x[got['index']] == got['value'], (h.label, s)
+            assert argmax_equiv(sc, int(got['index'])), (h.label, s)

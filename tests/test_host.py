@@ -152,3 +152,13 @@ def test_fmin_catch_eval_exceptions():
     with pytest.raises(RuntimeError):
         fmin(fn, hp.uniform('x', -1, 1), algo=rand.suggest, max_evals=10, trials=Trials(),
              rstate=np.random.RandomState(0))
+
+
+def test_seed_arrays_are_exact_uint64():
+    """Batch seeds above 2**63 mixed with small ones must not round through
+    float64 on their way to the engine."""
+    from hyperopt_amd._engine import _seeds
+    from hyperopt_amd.tpe import batch_seeds
+    s = batch_seeds(1234, 11)
+    assert [int(x) for x in _seeds(s)] == s
+    assert len(set(s)) == 11 and s[0] == 1234

@@ -153,3 +153,23 @@ def test_oracle_fmin_trajectories_equal_reference(name):
          algo=functools.partial(oracle_suggest, **kw), max_evals=n, trials=t,
          rstate=np.random.RandomState(123))
     assert trajectory(t) == ref['vals']
+
+
+def test_oracle_matches_reference_at_config4_size():
+    """K_a ~ 9976 (config 4): the oracle's lliks of the reference-drawn
+    candidates equal the reference's bit for bit (hps x0, x42)."""
+    from big_configs import cfg4_columns
+    meta = load_json('suggest_big_meta.json')['cfg4']
+    d = load('suggest_cfg4.npz')
+    U, L = cfg4_columns()
+    tids = np.arange(L.size)
+    for k, lab in enumerate(meta['labels']):
+        if lab not in ('x0', 'x42'):
+            continue
+        i = int(lab[1:])
+        bo, ao = O.split_observations(tids, U[:, i], tids, L, 0.25)
+        x = unpack(d, 'samples', k)
+        assert ao.size + 1 >= 9900
+        r = O.score_hp('uniform', (-5, 5), bo, ao, 1.0, x)
+        np.testing.assert_array_equal(r['llik_b'], unpack(d, 'llik_b', k))
+        np.testing.assert_array_equal(r['llik_a'], unpack(d, 'llik_a', k))

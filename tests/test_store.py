@@ -259,3 +259,19 @@ def test_fmin_batched_queue_uses_all_ids():
     H.fmin(lambda x: x, hp.uniform('x', 0, 1), algo=algo, max_evals=20, trials=t,
            rstate=np.random.RandomState(0), max_queue_len=4)
     assert len(t) == 20 and calls == [4] * 5
+
+
+def test_delete_all_and_refresh_cost_shape():
+    dom = Domain(lambda x: 0, SPACE)
+    t = Trials()
+    t.insert_trial_docs(rand.suggest([0, 1, 2], dom, t, 5))
+    t.refresh()
+    lst = t.trials
+    t.insert_trial_docs(rand.suggest([3], dom, t, 6))
+    t.refresh()
+    assert len(lst) == 3 and len(t.trials) == 4     # a new list per refresh
+    t.delete_all()
+    assert t.trials == [] and len(t) == 0
+    t.insert_trial_docs(rand.suggest([9], dom, t, 7))
+    t.refresh()
+    assert t.tids == [9]
