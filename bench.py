@@ -1,32 +1,38 @@
 #!/usr/bin/env python3
 """bench.py -- TPE candidate-scoring throughput of the MI355X engine.
 
-Metric (BASELINE.json): "EI candidates scored/sec (x components)" = (candidate,
-mixture-component) lpdf pairs per second, plus tpe.suggest latency.
+Metric (BASELINE.json): "EI candidates scored/sec (x components) +
+tpe.suggest latency".  ``value`` = (candidate, mixture-component) lpdf pairs
+of the whole job per second: for every active hyperparameter, candidates x
+(K_below + K_above), the work the reference's GMM1_lpdf / LGMM1_lpdf calls do
+(tpe.py:104-166, 259-301).  Pairs the engine proves to be exact zeros or
+reads off a value lattice are credited (their lpdf is produced) but not
+evaluated: ``evaluated_pairs_per_s`` reports the evaluated ones separately.
 
 One *step* = one whole device-side ``tpe.suggest`` posterior pass over the
 config's synthetic history, resident in HBM: good/bad split, both Parzen fits
 of every hyperparameter, Philox candidate draws, below/above lpdf of every
-candidate against every component, EI argmax.  Default workload: BASELINE
-configs[1] = config 2 (20-D mixed space, 1000-trial history, 4096 candidates).
+candidate, EI argmax.  Default workload: config 4 (BASELINE configs[3],
+100-D uniform space, 1e4-trial history, 1e7 candidates per hyperparameter),
+the largest single-GPU config.  --config cfg2 / cfg3 / cfg5 select the others.
 
---config cfg5 (BASELINE configs[4]: batched asynchronous suggestions x 1e6
-candidates, config 2's space and history): one step = one batch of --batch
-suggestions per rank in one engine call.
+Multi-GPU (one process per GPU; ``--gpus N`` without torchrun re-launches
+itself under torch.distributed.run before touching a GPU):
+* cfg4: the suggestion's candidates are sharded over ranks
+  (parallel.ShardedSuggest: per level an RCCL all-gather of 32-B records and
+  the device max-loc merge) -- strong scaling, fixed work per step;
+* cfg5: the batch of 1024 suggestions is split over ranks, no exchange --
+  strong scaling;
+* cfg2 / cfg3: each rank serves its own suggestion (replicas) -- weak.
 
-Multi-GPU (torch.distributed.run, one rank per GPU): weak scaling, each rank
-serves its own asynchronous suggestions (distinct seeds) on the shared
-history, no collective inside the timed region (batched suggestions shard
-with no data exchange; the in-suggest candidate sharding + RCCL max-loc path
-is hyperopt_amd/parallel.py:ShardedSuggest, covered by tests/test_parallel.py).
-
-Prints ONE JSON line on rank 0.
+Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -36,93 +42,223 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, 'tests'))
 
+CONFIGS = {
+    'cfg2': dict(n_cand=4096, batch=1, mode='replicas',
+                 desc='config 2: 20-D mixed space (uniform/loguniform/quniform/choice), '
+                      '1000-trial history, 4096 candidates/suggest'),
+    'cfg3': dict(n_cand=100_000, batch=1, mode='replicas',
+                 desc='config 3: 50-hp conditional space (nested choice, LGMM1 + '
+                      'categorical), 1e4-trial history, 1e5 candidates/suggest'),
+    'cfg4': dict(n_cand=10_000_000, batch=1, mode='sharded',
+                 desc='config 4: 100-D uniform space, 1e4-trial history, 1e7 '
+                      'candidates/suggest (lpdf roofline stress)'),
+    'cfg5': dict(n_cand=1_000_000, batch=1024, mode='batch',
+                 desc='config 5: 1024 batched asynchronous suggestions x 1e6 candidates '
+                      '(config 2 space + 1000-trial history)'),
+}
 
+
+# ----------------------------------------------------------------------------
+# workloads (host only)
+# ----------------------------------------------------------------------------
 def build_workload(cfg):
-    """(domain, losses, vals, active, n_cand, description)."""
+    """(domain, losses, vals[P, n], active[P, n])."""
     import spaces
+    import big_configs
     from hyperopt_amd import hp, rand, Trials
     from hyperopt_amd.base import Domain
     from hyperopt_amd.tpe import build_history
-    if cfg in ('cfg2', 'cfg5'):
+    if cfg == 'cfg4':
+        return big_configs.cfg4_domain_history(hp, Domain)
+    if cfg == 'cfg3':
+        dom, t = big_configs.cfg3_trials(hp, Domain, Trials, rand)
+    else:
         dom = Domain(lambda x: 0.0, spaces.cfg2_space(hp))
-        n_hist, n_cand = 1000, (4096 if cfg == 'cfg2' else 1_000_000)
-    elif cfg == 'cfg3':
-        dom = Domain(lambda x: 0.0, spaces.cfg3_space(hp))
-        n_hist, n_cand = 10000, 100000
-    elif cfg == 'cfg4':
-        dom = Domain(lambda x: 0.0, spaces.cfg4_space(hp))
-        n_hist, n_cand = 10000, 10_000_000
-    else:
-        raise ValueError(cfg)
-    losses = np.random.RandomState(2).rand(n_hist)
-    if cfg == 'cfg4':   # SURVEY 8(d): obs RandomState(1).uniform(-5,5,(1e4,100))
-        vals = np.random.RandomState(1).uniform(-5, 5, (n_hist, 100)).T.copy()
-        idx = np.array([int(l[1:]) for l in dom.space.labels])   # labels sort as strings
-        vals = np.ascontiguousarray(vals[idx])
-        active = np.ones_like(vals, dtype=np.uint8)
-    else:
-        docs = rand.suggest(list(range(n_hist)), dom, Trials(), 1)
-        for d, l in zip(docs, losses):
+        t = Trials()
+        docs = rand.suggest(list(range(1000)), dom, t, 1)
+        for d, l in zip(docs, np.random.RandomState(2).rand(1000)):
             d['state'] = 2
             d['result'] = {'status': 'ok', 'loss': float(l)}
-        from hyperopt_amd import trials_from_docs
-        t = trials_from_docs(docs, validate=False)
-        _, losses, vals, active = build_history(dom, t, dom.space.labels)
-    return dom, losses, vals, active, n_cand
+        t._insert_trial_docs(docs)
+        t.refresh()
+    _, losses, vals, active = build_history(dom, t, dom.space.labels)
+    return dom, losses, vals, active
 
 
-def cpu_baseline(dom, losses, vals, active, n_cand, budget_s):
-    """The oracle (numpy restatement, pinned to the reference) timed on one
-    host core over whole suggests of the bench's own space and history, with a
-    bounded candidate count (the reference path holds 8*n_c*K-byte temporaries,
-    so configs 3-5 cannot run at full n_c on the host); pairs as the GPU counts
-    them."""
-    os.environ.setdefault('OPENBLAS_NUM_THREADS', '1')
+# ----------------------------------------------------------------------------
+# CPU baseline: the oracle (numpy restatement pinned to the reference)
+# ----------------------------------------------------------------------------
+_CPU_CAND = {'cfg2': 4096, 'cfg3': 4096, 'cfg4': 128, 'cfg5': 4096}
+
+
+def _cpu_worker(args):
+    """Whole oracle suggests of the config's own space and history for
+    ``budget`` seconds (one process, one thread); returns (pairs, seconds,
+    suggests)."""
+    cfg, seed0, budget = args
+    os.environ['OPENBLAS_NUM_THREADS'] = '1'
     from oracle import tpe_oracle as O
-    import spaces
+    dom, losses, vals, active = build_workload('cfg2' if cfg == 'cfg5' else cfg)
     cs = dom.space
-    hps = {h.label: dict(dist=h.dist, args=h.args,
-                         conds=tuple(p for p in (h.paths[0] if h.paths else ()))) for h in cs.hps}
+    hps = {h.label: dict(dist=h.dist, args=h.args, paths=[tuple(p) for p in h.paths])
+           for h in cs.hps}
     tids = np.arange(losses.size)
     obs = {h.label: (tids[active[h.index] == 1], vals[h.index][active[h.index] == 1])
            for h in cs.hps}
-    runs, t_total, pairs = 0, 0.0, 0.0
+    n_c = _CPU_CAND[cfg]
+    runs, busy, pairs = 0, 0.0, 0.0
     with np.errstate(all='ignore'):
-        while t_total < budget_s or runs == 0:
+        while busy < budget or runs == 0:
             t0 = time.perf_counter()
-            chosen, det = O.suggest_reference_stream(hps, tids, losses, obs, 7 + runs,
-                                                     n_ei=n_cand)
-            t_total += time.perf_counter() - t0
+            _, det = O.suggest_reference_stream(hps, tids, losses, obs, seed0 + runs, n_ei=n_c)
+            busy += time.perf_counter() - t0
             runs += 1
             for lab, dd in det.items():
                 if cs.by_label[lab].is_categorical or len(dd['cand']) == 0:
                     continue
                 pairs += len(dd['cand']) * (len(dd['below'][0]) + len(dd['above'][0]))
-    return dict(value=pairs / t_total, unit='pairs/s', cores=1, kind='port',
-                sample='%d whole suggests of this config (%d candidates each) through the '
-                       'oracle (numpy/scipy float64 restatement of tpe.py, bit-equal to '
-                       'reference fixtures), single thread, %.1f s' % (runs, n_cand, t_total),
-                suggest_s=t_total / runs)
+    return pairs, busy, runs
+
+
+def cpu_baseline(cfg, n_cand, budget_s, cores):
+    """One core, then ``cores`` processes at once (independent suggests);
+    runs before any GPU call (spawned workers)."""
+    import multiprocessing as mp
+    one = _cpu_worker((cfg, 7, budget_s))
+    agg = None
+    if cores > 1:
+        ctx = mp.get_context('spawn')
+        t0 = time.perf_counter()
+        with ctx.Pool(cores) as pool:
+            res = pool.map(_cpu_worker, [(cfg, 1000 * (i + 1), budget_s) for i in range(cores)])
+        wall = time.perf_counter() - t0
+        # aggregate over the span every worker was computing (startup excluded)
+        span = max(r[1] for r in res)
+        agg = dict(pairs_per_s=sum(r[0] for r in res) / span, wall_s=wall,
+                   suggests=sum(r[2] for r in res))
+    n_c = _CPU_CAND[cfg]
+    sample = ('%d whole oracle suggests of this config\'s space and history (%d candidates '
+              'each%s); oracle = numpy/scipy float64 restatement of tpe.py, bit-equal to the '
+              'reference on the committed fixtures' % (
+                  one[2], n_c, '' if n_c == n_cand else ', a bounded sample of the %d' % n_cand))
+    out = dict(unit='pairs/s', kind='port', single_core=dict(value=one[0] / one[1], cores=1,
+                                                               suggest_s=one[1] / one[2]))
+    if agg is not None:
+        out.update(value=agg['pairs_per_s'], cores=cores,
+                   sample=sample + '; %d single-thread processes at once, %.0f s each, %d '
+                   'suggests in total' % (cores, budget_s, agg['suggests']))
+    else:
+        out.update(value=one[0] / one[1], cores=1, sample=sample)
+    return out
+
+
+def host_cores():
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))      # the GPU box's CPU share is 16
+
+
+# ----------------------------------------------------------------------------
+# end-to-end tpe.suggest latency (host call -> returned trial document)
+# ----------------------------------------------------------------------------
+def e2e_latency(cfg, n_calls):
+    """tpe.suggest through a real Trials in an fmin-like loop: each call sees
+    one more finished trial (incremental columnar history + one engine
+    call); returns median / p90 ms and the host share."""
+    import spaces
+    import big_configs
+    from hyperopt_amd import hp, rand, tpe, Trials
+    from hyperopt_amd.base import Domain
+    if cfg == 'cfg3':
+        dom, t = big_configs.cfg3_trials(hp, Domain, Trials, rand)
+        n_c = CONFIGS['cfg3']['n_cand']
+    else:
+        dom = Domain(lambda x: 0.0, spaces.cfg2_space(hp))
+        t = Trials()
+        docs = rand.suggest(list(range(1000)), dom, t, 1)
+        for d, l in zip(docs, np.random.RandomState(2).rand(1000)):
+            d['state'] = 2
+            d['result'] = {'status': 'ok', 'loss': float(l)}
+        t._insert_trial_docs(docs)
+        t.refresh()
+        n_c = CONFIGS['cfg2']['n_cand']
+    rng = np.random.RandomState(5)
+    tpe.suggest(t.new_trial_ids(1), dom, t, 1, n_EI_candidates=n_c)   # builds plan + mirror
+    st = dom._tpe_state
+    lat, host = [], []
+    for i in range(n_calls):
+        ids = t.new_trial_ids(1)
+        t0 = time.perf_counter()
+        docs = tpe.suggest(ids, dom, t, 100 + i, n_EI_candidates=n_c)
+        t1 = time.perf_counter()
+        lat.append(t1 - t0)
+        # host-only part: the history sync + row upload of the same call
+        h = st.histories[t]
+        t2 = time.perf_counter()
+        h.sync(t)
+        t3 = time.perf_counter()
+        host.append(t3 - t2)
+        t.insert_trial_docs(docs)
+        t.refresh()
+        t.trials[-1]['result'] = {'status': 'ok', 'loss': float(rng.rand())}
+        t.trials[-1]['state'] = 2
+    lat = 1e3 * np.asarray(lat)
+    return dict(tpe_suggest_ms_median=float(np.median(lat)),
+                tpe_suggest_ms_p90=float(np.percentile(lat, 90)),
+                history_sync_ms_median=float(1e3 * np.median(host)),
+                calls=n_calls, candidates=n_c, history=len(t.trials) - n_calls,
+                note='hyperopt_amd.tpe.suggest on a real Trials, host call to returned doc, '
+                     'one new finished trial between calls (tpe.py:804-897 boundary, '
+                     'fmin.py:155-156)')
+
+
+# ----------------------------------------------------------------------------
+def _launch_ranks(n):
+    """Re-launch under torch.distributed.run (child process; no GPU touched yet)."""
+    import socket
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+           '--nproc-per-node=%d' % n, '--master-addr=127.0.0.1', '--master-port=%d' % port,
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=50)
-    ap.add_argument('--warmup', type=int, default=10)
-    ap.add_argument('--config', default='cfg2', choices=['cfg2', 'cfg3', 'cfg4', 'cfg5'])
-    ap.add_argument('--batch', type=int, default=0,
-                    help='suggestions per rank per step (default 1; cfg5: 16)')
-    ap.add_argument('--cpu-seconds', type=float, default=12.0)
+    ap.add_argument('--steps', type=int, default=5)
+    ap.add_argument('--warmup', type=int, default=1)
+    ap.add_argument('--config', default='cfg4', choices=sorted(CONFIGS))
+    ap.add_argument('--batch', type=int, default=16,
+                    help='cfg5: suggestions per engine call')
     ap.add_argument('--n-cand', type=int, default=0,
                     help='override candidates per suggest (secondary measurements only)')
+    ap.add_argument('--cpu-seconds', type=float, default=10.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-e2e', action='store_true')
     ap.add_argument('--traffic-json', default=os.path.join(ROOT, 'profiles', 'traffic.json'))
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
+    if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
+        sys.exit(_launch_ranks(args.gpus))
+    if world != args.gpus:
+        print('bench.py: --gpus %d but WORLD_SIZE=%d' % (args.gpus, world), file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    C = CONFIGS[args.config]
+    n_cand = args.n_cand or C['n_cand']
+
+    # CPU baseline first (rank 0, N = 1): host processes only, before any GPU call
+    cpu = None
+    if not args.no_cpu_baseline and world == 1:
+        cpu = cpu_baseline(args.config, n_cand, args.cpu_seconds, host_cores())
+
     import torch
     torch.cuda.set_device(local)
     dist = None
@@ -131,11 +267,9 @@ def main():
         dist.init_process_group('nccl', device_id=torch.device('cuda', local))
 
     from hyperopt_amd import _engine as E
-    eng = E.Engine(local)
-    dom, losses, vals, active, n_cand = build_workload(args.config)
-    if args.n_cand:
-        n_cand = args.n_cand
-    batch = args.batch or (16 if args.config == 'cfg5' else 1)
+    from hyperopt_amd import parallel, tpe
+    eng = E.default_engine(local)
+    dom, losses, vals, active = build_workload(args.config)
     hps, conds, pprior = dom.space.engine_tables()
     plan = E.Plan(eng, hps, conds, pprior, max_trials=losses.size)
     # history resident in HBM before the timed region
@@ -146,11 +280,24 @@ def main():
     plan.set_history_device(d_losses.data_ptr(), d_vals.data_ptr(), d_act.data_ptr(),
                             losses.size)
 
+    mode = C['mode'] if world > 1 else 'single'
+    sharded = parallel.ShardedSuggest(plan) if mode == 'sharded' else None
+    if args.config == 'cfg5':
+        mine = list(parallel.suggestion_slice(C['batch'], rank, world))
+    else:
+        mine = [0]
+
     def step(i):
-        # fit + suggest in one engine call (a replayed hipGraph after the first
-        # call of this shape); results stay device-resident in the plan
-        seeds = [1_000_003 * rank + 4099 * i + 17 * b + 7 for b in range(batch)]
-        plan.fit_suggest(seeds, n_cand, gamma=0.25, prior_weight=1.0, lf=25, fetch=False)
+        if sharded is not None:
+            plan.fit()
+            sharded.suggest([7 + 4099 * i], n_cand, fetch=False)
+            return
+        if args.config == 'cfg5':
+            for b0 in range(0, len(mine), args.batch):
+                seeds = [1_000_003 * (i + 1) + s for s in mine[b0:b0 + args.batch]]
+                plan.fit_suggest(seeds, n_cand, fetch=False)
+            return
+        plan.fit_suggest([1_000_003 * rank + 4099 * i + 7], n_cand, fetch=False)
 
     for i in range(args.warmup):
         step(i)
@@ -164,18 +311,31 @@ def main():
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
+    torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device='cuda')
+    tt = torch.tensor([elapsed], dtype=torch.float64, device='cuda')
     if dist:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
-    _, pairs_step = plan.last_stats()
-    value = world * pairs_step * args.steps / elapsed
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    elapsed = float(tt.item())
+
+    # logical pairs of one suggestion (whole candidate set) from this rank's
+    # last engine call: its pairs per candidate x the full candidate count
+    _, last_pairs = plan.last_stats()
+    per_call_cand = plan_last_cand(plan)
+    pairs_suggest = last_pairs / max(1, per_call_cand) * n_cand / max(1, plan._last_nsug)
+    if mode == 'replicas':
+        sug_step = world
+    elif mode == 'batch' or args.config == 'cfg5':
+        sug_step = C['batch']
+    else:
+        sug_step = 1
+    pairs_step = pairs_suggest * sug_step
+    value = pairs_step * args.steps / elapsed
 
     # ---- profiled pass (after the timed region): HIP events on the engine
-    # stream around every scoring launch, and the quantized-pair census
-    n_prof = max(1, min(args.steps, 20))
-    plan.profile(n_prof * 64)   # event ring: every scoring launch of every profiled step
+    # stream around every scoring / lattice launch, and the pair census
+    n_prof = 1 if args.config in ('cfg4', 'cfg5') else max(1, min(args.steps, 20))
+    plan.profile(n_prof * 4096)
     for i in range(n_prof):
         step(args.warmup + args.steps + i)
     kinds = {}
@@ -187,54 +347,50 @@ def main():
             kinds[name] = pairs
     lat_ms, lat_launches, lat_pairs = plan.profile_read(5)
     plan.profile(0)
-    # A/B: the same steps with every quantized candidate scored on its own
-    # (no value lattice), timed like the main region
-    no_lat = None
-    if lat_launches and args.config == "cfg2":
-        plan.set_lattice(False)
-        for i in range(max(1, args.warmup)):
-            step(i)
-        torch.cuda.synchronize()
-        if dist:
-            dist.barrier()
-        t1 = time.perf_counter()
-        for i in range(args.steps):
-            step(args.warmup + i)
-        torch.cuda.synchronize()
-        if dist:
-            dist.barrier()
-        e1 = time.perf_counter() - t1
-        t = torch.tensor([e1], dtype=torch.float64, device='cuda')
-        if dist:
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        e1 = float(t.item())
-        no_lat = dict(value=world * pairs_step * args.steps / e1, ms_per_step=1e3 * e1 / args.steps)
-        plan.set_lattice(True)
-    # census pass (its counting variant of the kernel is not timed)
     plan.census(True)
     for i in range(n_prof):
         step(args.warmup + args.steps + n_prof + i)
     census = plan.census(False)
 
+    e2e = None
+    if rank == 0 and world == 1 and not args.no_e2e:
+        e2e = dict(cfg2=e2e_latency('cfg2', 30), cfg3=e2e_latency('cfg3', 10))
+
     if rank != 0:
         if dist:
             dist.destroy_process_group()
         return
-    # ---- roofline of the dominant kernel, k_score (every lpdf kind of the
-    # level in one launch).  Work is priced at the measured register-only
-    # rate of exactly its pair arithmetic: log-sum-exp pairs (2 FMA + max +
-    # exp2 + fp64 sum) and evaluated quantized pairs (2 fp64 erf); quantized
-    # pairs that are exact zeros for the whole wave are skipped by the
-    # algorithm and cost no erf.
+    line = report(args, C, eng, world, mode, elapsed, value, pairs_step, pairs_suggest,
+                  sug_step, n_cand, kinds, score_ms, launches, n_prof, lat_ms, lat_launches,
+                  lat_pairs, census, cpu, e2e)
+    print(json.dumps(line))
+    if dist:
+        dist.destroy_process_group()
+
+
+def plan_last_cand(plan):
+    """Candidates per suggestion of the plan's last engine call (a shard in
+    sharded mode)."""
+    return int(getattr(plan, '_last_ncand', 0)) or 1
+
+
+def report(args, C, eng, world, mode, elapsed, value, pairs_step, pairs_suggest, sug_step,
+           n_cand, kinds, score_ms, launches, n_prof, lat_ms, lat_launches, lat_pairs, census,
+           cpu, e2e):
+    from hyperopt_amd import _engine as E
+    # roofline of the dominant kernel, k_score (every lpdf kind of a level
+    # in one launch), priced at the measured register-only rate of exactly
+    # its pair arithmetic (k_micro): log-sum-exp pairs and evaluated
+    # quantized pairs (the per-wave exact-zero skips cost no erf)
     lse_peak = eng.microbench(3)
     erf_peak = eng.microbench(4)
     lse_pairs = kinds.get('lse_gmm', 0.0) + kinds.get('lse_lgmm', 0.0)
-    erf_pairs = kinds.get('erf_gmm', 0.0) + kinds.get('erf_lgmm', 0.0)
     per_launch = max(1, launches)
+    lse_exec = census[5] / per_launch if census[3] else lse_pairs
     erf_exec = census[2] / per_launch
     t_kernel = score_ms * 1e-3
-    t_peak = lse_pairs / lse_peak + erf_exec / erf_peak
-    achieved = (lse_pairs + erf_exec * lse_peak / erf_peak) / t_kernel if t_kernel else 0.0
+    t_peak = lse_exec / lse_peak + erf_exec / erf_peak
+    achieved = (lse_exec + erf_exec * lse_peak / erf_peak) / t_kernel if t_kernel else 0.0
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
@@ -242,73 +398,64 @@ def main():
                 traffic = json.load(f).get(args.config, {}).get('score')
         except Exception:
             traffic = None
+    steps_per_launch = launches / n_prof if n_prof else 0
+    lat_pairs_step = lat_pairs * (lat_launches / n_prof if n_prof else 0)
+    eval_step = (lse_exec + erf_exec) * steps_per_launch + lat_pairs_step
     roof = dict(bound='valu', unit='Gpair/s', achieved=achieved / 1e9, peak=lse_peak / 1e9,
                 frac=(t_peak / t_kernel) if t_kernel else None, traffic=traffic,
                 kernel='k_score (all lpdf kinds of a level, one launch)',
-                avg_launch_ms=score_ms, launches_per_step=launches / n_prof,
-                note='unit = log-sum-exp-pair equivalents: achieved = (LSE pairs + evaluated '
-                     'quantized pairs x lse_peak/erf_peak) / launch time; peaks are '
+                avg_launch_ms=score_ms, launches_per_step=steps_per_launch,
+                note='unit = log-sum-exp-pair equivalents: achieved = (evaluated LSE pairs + '
+                     'evaluated quantized pairs x lse_peak/erf_peak) / launch time; peaks are '
                      'register-only microkernels of exactly the pair arithmetic (LSE pair: 2 '
                      'fp64 FMA + max + v_exp_f32 + fp64 sum, SURVEY 8d "1 exp + 6 flops"; '
                      'quantized pair: 2 OCML fp64 erf + 8 flops)',
-                lse_pairs_per_launch=lse_pairs, erf_pairs_per_launch=erf_pairs,
-                erf_live_pairs_per_launch=census[1] / per_launch,
+                lse_pairs_per_launch=lse_pairs, lse_evaluated_pairs_per_launch=lse_exec,
+                erf_pairs_per_launch=kinds.get('erf_gmm', 0.0) + kinds.get('erf_lgmm', 0.0),
                 erf_evaluated_pairs_per_launch=erf_exec,
                 lse_pair_peak_per_s=lse_peak, erf_pair_peak_per_s=erf_peak,
                 fp64_fma_peak_flops=eng.microbench(1), exp_f32_peak_per_s=eng.microbench(0),
                 erf_f64_peak_per_s=eng.microbench(2))
-
-    if lat_launches and args.config == "cfg2":
+    if lat_launches:
         roof['lattice'] = dict(
             kernel='k_lattice (bounded quantized hps: every lattice value j*q scored once per '
-                   'suggest call, candidates look their lpdfs up in k_score; bit-identical; for '
-                   'small draws the launch also carries the candidate-draw blocks, timed with it)',
+                   'call; candidates look their lpdfs up in k_score; bit-identical)',
             avg_launch_ms=lat_ms, launches_per_step=lat_launches / n_prof,
-            pairs_per_launch=lat_pairs,
-            erf_pair_rate_per_s=lat_pairs / (lat_ms * 1e-3) if lat_ms else None,
-            frac_of_erf_pair_peak=(lat_pairs / (lat_ms * 1e-3)) / erf_peak if lat_ms else None)
-    cpu = None
-    if not args.no_cpu_baseline and world == 1:
-        n_cpu = {'cfg2': n_cand, 'cfg3': 4096, 'cfg4': 128, 'cfg5': 4096}[args.config]
-        cpu = cpu_baseline(dom, losses, vals, active, n_cpu, args.cpu_seconds)
-        if n_cpu != n_cand:
-            cpu['sample'] += ' (bounded sample: %d of %d candidates per suggest)' % (n_cpu, n_cand)
-
-    line = {
+            pairs_per_launch=lat_pairs)
+    ms_step = 1e3 * elapsed / args.steps
+    return {
         'metric': 'EI candidates scored/sec (x components)',
         'value': value,
         'unit': 'pairs/s',
         'n_gpus': world,
         'steps': args.steps,
         'warmup': args.warmup,
-        'ms_per_step': 1e3 * elapsed / args.steps,
+        'ms_per_step': ms_step,
         'higher_is_better': True,
-        'scaling': 'weak',
+        'scaling': 'weak' if mode == 'replicas' else 'strong',
         'vs_baseline': None,
-        'dtype': 'f64',
-        'data': 'synthetic (rand.suggest startup history, RandomState(2) losses)',
+        'dtype': 'f64 (log-sum-exp: fp64 exponent and accumulation, fp32 exp2 of the '
+                 'shifted term; quantized: fp64 erf)',
+        'data': 'synthetic (SURVEY 8(d) histories: RandomState seeds as in tests/big_configs.py)',
         'config': {
-            'workload': {'cfg2': 'config 2: 20-D mixed space, 1000-trial history, 4096 '
-                                 'candidates/suggest', 'cfg3': 'config 3: 50-hp conditional, '
-                                 '1e4 history, 1e5 candidates', 'cfg4': 'config 4: 100-D, 1e4 '
-                                 'history, 1e7 candidates',
-                         'cfg5': 'config 5: batched asynchronous suggestions x 1e6 candidates '
-                                 '(config 2 space + 1000-trial history), %d suggestions per GPU '
-                                 'per step' % batch}[args.config],
-            'suggestions_per_step_per_gpu': batch,
+            'workload': C['desc'],
+            'parallelism': {'single': 'single', 'sharded': 'cand-sharded%d' % world,
+                            'batch': 'batch-sharded%d' % world,
+                            'replicas': 'replicas%d' % world}[mode],
             'candidates_per_suggest': n_cand,
+            'suggestions_per_step': sug_step,
             'pairs_per_step': pairs_step,
-            'pairs_per_suggest': pairs_step / batch,
-            'suggest_latency_ms': 1e3 * elapsed / args.steps / batch,
-            'parallelism': 'replicas' if world > 1 else 'single',
+            'pairs_per_suggest': pairs_suggest,
+            'suggest_latency_ms': ms_step / sug_step if mode != 'replicas' else ms_step,
         },
+        'evaluated_pairs_per_s': eval_step * sug_step / (ms_step * 1e-3) if ms_step else None,
+        'evaluated_pairs_note': 'pairs actually computed per step: log-sum-exp pairs outside '
+                                'the provably-zero component blocks, quantized pairs not '
+                                'skipped as exact zeros, and value-lattice points x components',
         'roofline': roof,
-        'per_candidate_quantized': no_lat,
+        'e2e': e2e,
         'cpu_baseline': cpu,
     }
-    print(json.dumps(line))
-    if dist:
-        dist.destroy_process_group()
 
 
 if __name__ == '__main__':

@@ -39,7 +39,7 @@ EXPORTS = (
     'tpe_plan_suggest', 'tpe_plan_merge', 'tpe_plan_score_candidates', 'tpe_plan_last_stats',
     'tpe_plan_profile', 'tpe_plan_profile_read', 'tpe_microbench', 'tpe_plan_get_results',
     'tpe_plan_results_device', 'tpe_plan_census', 'tpe_plan_fit_suggest',
-    'tpe_plan_set_lattice', 'tpe_plan_update_history',
+    'tpe_plan_set_lattice', 'tpe_plan_update_history', 'tpe_plan_set_prune',
 )
 
 
@@ -145,6 +145,7 @@ def load_library(path: str = LIB_PATH):
             'tpe_plan_results_device': (vp, [vp]),
             'tpe_plan_census': (C.c_int, [vp, i32, C.POINTER(i64)]),
             'tpe_plan_set_lattice': (C.c_int, [vp, i32]),
+            'tpe_plan_set_prune': (C.c_int, [vp, i32]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -417,6 +418,7 @@ class Plan(object):
                                            seeds.size, int(n_cand), int(cand_begin), int(level),
                                            optr, 0 if host else 1, stream))
         self._last_nsug = seeds.size
+        self._last_ncand = int(n_cand)
         return res
 
     def fit_suggest(self, seeds, n_cand, gamma=0.25, prior_weight=1.0, lf=25, gamma_cap=25,
@@ -434,6 +436,7 @@ class Plan(object):
                 seeds.ctypes.data_as(C.POINTER(C.c_uint64)), seeds.size, int(n_cand),
                 optr, 0 if host else 1, stream))
         self._last_nsug = seeds.size
+        self._last_ncand = int(n_cand)
         return res
 
     def results(self):
@@ -487,11 +490,19 @@ class Plan(object):
         with e.lock:
             e.check(e.lib.tpe_plan_set_lattice(self.p, int(bool(enable))))
 
-    def census(self, enable):
-        """Quantized-pair census since the last call (total, live, evaluated);
-        enable it for the following suggests."""
+    def set_prune(self, enable):
+        """Skip provably-zero log-sum-exp component blocks on bucketed large
+        draws (default) or evaluate every pair (tpe_plan_set_prune)."""
         e = self.engine
-        out = (C.c_int64 * 3)()
+        with e.lock:
+            e.check(e.lib.tpe_plan_set_prune(self.p, int(bool(enable))))
+
+    def census(self, enable):
+        """Pair census since the last call: (quantized total, live, evaluated,
+        log-sum-exp total, 0, log-sum-exp evaluated); enable it for the
+        following suggests."""
+        e = self.engine
+        out = (C.c_int64 * 6)()
         with e.lock:
             e.check(e.lib.tpe_plan_census(self.p, int(bool(enable)), out))
         return tuple(int(v) for v in out)

@@ -115,4 +115,39 @@ __device__ __forceinline__ Coef make_coef(const tpe_hp &H, double w, double mu, 
   return c;
 }
 
+// The log-sum-exp envelope of coefficient block b (components [8b, 8b+8) of
+// K) of a continuous mixture, written into the block's w-row as 4 floats
+// (tpe_internal.hpp, kLseDead).  Same c and a^2 as make_coef.
+__device__ __forceinline__ void store_lse_envelope(const tpe_hp &H, Coef *table, int b, int K,
+                                                   const double *w, const double *mu,
+                                                   const double *sg, double pacc) {
+#pragma clang fp contract(off)
+  const double L2E = 1.4426950408889634;
+  double lo = INFINITY, hi = -INFINITY, cmax = -INFINITY, amin = INFINITY;
+  for (int k = b * kCoefBlock; k < min(K, (b + 1) * kCoefBlock); ++k) {
+    const double sp = np_maximum(sg[k], kEPS);
+    double cc;
+    if (H.family == TPE_GMM) {
+      const double Z = sqrt(2.0 * 3.141592653589793 * (sg[k] * sg[k]));
+      cc = L2E * log(w[k] / Z / pacc);
+    } else {
+      cc = L2E * (log(w[k]) - log(sp * 2.5066282746310002));
+    }
+    const double a2 = (0.5 * L2E) / (sp * sp);
+    const double m = mu[k] - H.prior_mu;
+    lo = fmin(lo, m);
+    hi = fmax(hi, m);
+    cmax = (cc == cc) ? fmax(cmax, cc) : INFINITY;  // a NaN term: never skip
+    amin = fmin(amin, a2);
+  }
+  // outward fp32 rounding: the float box contains the exact one
+  float *e = reinterpret_cast<float *>(reinterpret_cast<double *>(table) + coef_off(b * kCoefBlock, 3));
+  const float flo = (float)lo, fhi = (float)hi, fc = (float)cmax, fa = (float)amin;
+  e[0] = ((double)flo > lo) ? nextafterf(flo, -INFINITY) : flo;
+  e[1] = ((double)fhi < hi) ? nextafterf(fhi, INFINITY) : fhi;
+  e[2] = ((double)fc < cmax) ? nextafterf(fc, INFINITY) : fc;
+  e[3] = ((double)fa > amin) ? nextafterf(fa, 0.0f) : fa;
+  if (!(amin == amin) || !(lo == lo) || !(hi == hi)) { e[2] = INFINITY; e[3] = 0.0f; }
+}
+
 }  // namespace tpe

@@ -61,7 +61,7 @@ struct tpe_plan {
   uint64_t *d_seeds = nullptr;
   Partial *d_partial = nullptr;
   size_t partial_cap = 0;
-  unsigned long long *d_census = nullptr;  // [3] quantized-pair census (tpe_plan_census)
+  unsigned long long *d_census = nullptr;  // [kCensus] pair census (tpe_plan_census)
   bool census = false;
   uint32_t *d_ticket = nullptr;
   std::vector<uint64_t> h_seeds;  // this call's seeds (inline kernel args when <= 8)
@@ -71,6 +71,7 @@ struct tpe_plan {
   LatInfo *d_lat_info = nullptr;
   double2 *d_lat = nullptr;
   bool lattice_on = true;
+  bool prune_on = true;  // skip provably-zero log-sum-exp blocks (tpe_plan_set_prune)
   hipEvent_t ev_fork = nullptr, ev_join[8] = {};
   double *d_ext = nullptr, *d_lb = nullptr, *d_la = nullptr;
   size_t ext_cap = 0;
@@ -333,8 +334,8 @@ int plan_build(tpe_engine *h, const tpe_space *sp, int64_t max_trials, tpe_plan 
   p->scap = p->ncap + 1;
   CKH(dalloc(&p->d_sortbuf, (size_t)slots * 16 * p->scap));
   CKH(dalloc(&p->d_info, slots));
-  CKH(dalloc(&p->d_census, 3));
-  CKH(hipMemset(p->d_census, 0, 3 * sizeof(unsigned long long)));
+  CKH(dalloc(&p->d_census, kCensus));
+  CKH(hipMemset(p->d_census, 0, kCensus * sizeof(unsigned long long)));
   CKH(dalloc(&p->d_coef, (size_t)slots * kcap));
   CKH(hipEventCreate(&p->ev0));
   CKH(hipEventCreate(&p->ev1));
@@ -644,6 +645,13 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
     a.cand_slot0 = 0;
     for (int i = 0; i < kInlineSeeds && i < n_sug; ++i) a.seed_inline[i] = p->h_seeds[i];
     a.n_inline_seeds = (int32_t)std::min<int64_t>(n_sug, kInlineSeeds);
+    // large draws: each draw block writes its candidates value-bucketed (LSE
+    // and per-candidate erf slots) with their positions; the log-sum-exp
+    // tiles then skip the component blocks that are exact zeros for them
+    const bool sorted_draw = !fuse_draw && table_draw &&
+                             cn * n_sug * n_level >= ((int64_t)1 << 22);
+    a.lse_pos = sorted_draw ? 1 : 0;
+    a.lse_prune = (sorted_draw && p->prune_on) ? 1 : 0;
     if (fuse_draw) {
       tpe_plan::Prof *pr = nullptr;
       if (p->prof_cap > 0 && p->prof[1].n < p->prof_cap) pr = &p->prof[1];
@@ -655,11 +663,13 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
         pr->pairs[pr->n] = (double)level;
         pr->n++;
       }
+    } else if (sorted_draw) {
+      CKH(launch_draw_sorted(a, kmax <= kFuseTab, p->d_cpos, st));
     } else {
       CKH(launch_draw(a, table_draw, st));
     }
-    if (erf_level) CKH(launch_bucket(a, n_lat, p->d_cpos, st));
-    a.cand_pos = erf_level ? p->d_cpos : nullptr;
+    if (erf_level && !sorted_draw) CKH(launch_bucket(a, n_lat, p->d_cpos, st));
+    a.cand_pos = (erf_level || sorted_draw) ? p->d_cpos : nullptr;
     if (!joined) {
       CKH(hipStreamWaitEvent(st, p->ev_join[0], 0));
       joined = true;
@@ -1197,13 +1207,18 @@ int launch_step(tpe_engine *h, tpe_plan *p, int32_t nb, const uint64_t *seeds, i
     for (int64_t j = 0; j < n_sug; ++j) da.seed_inline[j] = seeds[j];
     da.n_inline_seeds = (int32_t)n_sug;
     hipKernelNodeParams kp = p->draw_params[i];
-    // k_lattice<true> (fused draw) also takes its jobs and output pointer
+    // k_lattice<true> (fused draw) also takes its jobs and output pointer,
+    // k_draw_sorted its position buffer
     LatJobs jobs{};
     double2 *lat_out = nullptr;
+    int32_t *pos_out = nullptr;
     void *args[3] = {&da, &jobs, &lat_out};
     if (kp.func == lattice_draw_kernel_fn()) {
       jobs = *static_cast<const LatJobs *>(kp.kernelParams[1]);
       lat_out = *static_cast<double2 *const *>(kp.kernelParams[2]);
+    } else if (is_sorted_draw_kernel_fn(kp.func)) {
+      pos_out = *static_cast<int32_t *const *>(kp.kernelParams[1]);
+      args[1] = &pos_out;
     }
     kp.kernelParams = args;
     kp.extra = nullptr;
@@ -1421,12 +1436,19 @@ int tpe_plan_census(tpe_plan_t p, int32_t enable, int64_t *counts) {
   CKH(hipSetDevice(h->device));
   CKH(hipDeviceSynchronize());
   if (counts) {
-    unsigned long long c[3];
+    unsigned long long c[kCensus];
     CKH(hipMemcpy(c, p->d_census, sizeof(c), hipMemcpyDeviceToHost));
-    for (int i = 0; i < 3; ++i) counts[i] = (int64_t)c[i];
+    for (int i = 0; i < kCensus; ++i) counts[i] = (int64_t)c[i];
   }
-  CKH(hipMemset(p->d_census, 0, 3 * sizeof(unsigned long long)));
+  CKH(hipMemset(p->d_census, 0, kCensus * sizeof(unsigned long long)));
   p->census = enable != 0;
+  return TPE_OK;
+}
+
+int tpe_plan_set_prune(tpe_plan_t p, int32_t enable) {
+  if (!p) return TPE_E_INVALID;
+  if (p->prune_on != (enable != 0)) graph_reset(p);
+  p->prune_on = enable != 0;
   return TPE_OK;
 }
 

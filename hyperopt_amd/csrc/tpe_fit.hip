@@ -662,6 +662,7 @@ __device__ void prep_slot(const tpe_hp &H, int64_t slot, int K, const double *w,
     if (threadIdx.x == 0) {
       MixInfo mi;
       mi.K = K; mi.kind = 2; mi.p_accept = 1.0; mi.log_pacc = 0.0; mi.wsum = wsum;
+      mi.probe = -1; mi.pad = 0;
       info[slot] = mi;
     }
     return;
@@ -677,11 +678,14 @@ __device__ void prep_slot(const tpe_hp &H, int64_t slot, int K, const double *w,
   STAMP(8);
   const bool quant = (H.flags & TPE_HAS_Q) != 0;
   for (int k = threadIdx.x; k < K; k += blockDim.x)
-    store_coef(cf, k, make_coef(H, w[k], mu[k], sg[k], pacc));
+    store_coef(cf, k, make_coef(H, w[k], mu[k], sg[k], pacc), quant);
+  if (!quant)
+    for (int b = threadIdx.x; b * kCoefBlock < K; b += blockDim.x)
+      store_lse_envelope(H, cf, b, K, w, mu, sg, pacc);
   if (threadIdx.x == 0) {
     MixInfo mi;
     mi.K = K; mi.kind = quant ? 1 : 0; mi.p_accept = pacc; mi.log_pacc = log(pacc);
-    mi.wsum = wsum;
+    mi.wsum = wsum; mi.probe = -1; mi.pad = 0;
     info[slot] = mi;
   }
 }
@@ -779,13 +783,18 @@ __device__ void fit_continuous(const FitArgs &A, const FitCtx &C, FitShared &sm,
   Coef *cf = A.coef + slot * A.kcap;
   for (int k = threadIdx.x; k < K; k += blockDim.x) {
     const double s = sg[k], wk = w[k], mk = mu[k];
-    store_coef(cf, k, make_coef(H, wk, mk, s, pacc));
+    store_coef(cf, k, make_coef(H, wk, mk, s, pacc), quant);
     if (MIXLDS) { gw[k] = wk; gm[k] = mk; gs[k] = s; }
   }
+  if (!quant)
+    for (int b = threadIdx.x; b * kCoefBlock < K; b += blockDim.x)
+      store_lse_envelope(H, cf, b, K, w, mu, sg, pacc);
   if (threadIdx.x == 0) {
     MixInfo mi;
     mi.K = K; mi.kind = quant ? 1 : 0; mi.p_accept = pacc; mi.log_pacc = log(pacc);
     mi.wsum = wsum;
+    mi.probe = pos;  // the prior: sigma = prior_sigma, the widest after the clip
+    mi.pad = 0;
     A.info[slot] = mi;
   }
 }

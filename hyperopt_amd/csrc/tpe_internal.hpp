@@ -45,7 +45,23 @@ struct MixInfo {
   double p_accept;  // truncation mass (tpe.py:130-136, 273-276)
   double log_pacc;  // log(p_accept) subtracted by the quantized lpdf
   double wsum;      // sum of weights (sampler CDF total)
+  int32_t probe;    // LSE: a widest component (the Parzen prior), whose term
+                    // lower-bounds every candidate's log-sum-exp maximum; -1: none
+  int32_t pad;
 };
+
+// Log-sum-exp block envelope (LSE kinds): in the spare w-row of every
+// coefficient block, 4 floats bounding the block's terms
+//   [0] min mu', [1] max mu' (rounded outward), [2] max c (log2 units,
+//   rounded up), [3] min a^2 (rounded down),
+// so t_k(y') <= c_max - a2_min * dist(y', [mu'_lo, mu'_hi])^2 for every
+// component k of the block.  The scoring kernel skips a block whose bound,
+// over the wave's candidate range, is below (lower bound of the lane maxima)
+// - kLseDead: its terms are exact zeros of the fp32 exp2.
+constexpr float kLseDead = 151.0f;
+// census counters (tpe_plan_census): quantized total / live / evaluated,
+// log-sum-exp total / (reserved) / evaluated
+constexpr int kCensus = 6;
 
 // Per-component scoring coefficients (make_coef, tpe_device.hpp), 4 fields:
 //   LSE: x = alpha, y = beta, z = gamma (t = alpha + y'(beta + gamma y'))
@@ -63,12 +79,14 @@ constexpr int kCoefBlock = 8;
 __host__ __device__ constexpr int64_t coef_off(int64_t k, int f) {
   return (k / kCoefBlock) * (4 * kCoefBlock) + f * kCoefBlock + (k % kCoefBlock);
 }
-__device__ __forceinline__ void store_coef(Coef *table, int64_t k, const Coef &c) {
+// with_w false (log-sum-exp kinds): the w-row holds the block envelope instead
+__device__ __forceinline__ void store_coef(Coef *table, int64_t k, const Coef &c,
+                                           bool with_w = true) {
   double *t = reinterpret_cast<double *>(table);
   t[coef_off(k, 0)] = c.x;
   t[coef_off(k, 1)] = c.y;
   t[coef_off(k, 2)] = c.z;
-  t[coef_off(k, 3)] = c.w;
+  if (with_w) t[coef_off(k, 3)] = c.w;
 }
 
 struct Partial {  // == tpe_result layout
@@ -131,7 +149,9 @@ struct ScoreArgs {
   int32_t grp_block0[kMaxGroups + 1];  // first block of each group; [n_groups] = total
   int32_t force_active;      // ignore conditions (operator-level scoring)
   int32_t accumulate;        // merge with results of an earlier candidate chunk
-  unsigned long long *census;  // optional [3]: quantized pairs total / live / executed
+  unsigned long long *census;  // optional [kCensus] pair counters (tpe_plan_census)
+  int32_t lse_pos;           // LSE slots' candidates are value-bucketed (cand_pos valid)
+  int32_t lse_prune;         // skip log-sum-exp blocks of exact-zero terms (needs lse_pos)
   const LatInfo *lat_info;   // [P] value lattices (KIND_LAT slots)
   const double2 *lat;        // lattice (lpdf below, lpdf above) pairs
 };
@@ -162,7 +182,8 @@ struct FitArgs {
 hipError_t launch_split(const FitArgs &a, uint8_t *below, hipStream_t st);
 hipError_t launch_fit(const FitArgs &a, int32_t n_hp, hipStream_t st);
 const void *fit_kernel_fn();               // k_fit's host stub (graph node lookup)
-bool is_draw_kernel_fn(const void *f);     // one of k_draw's host stubs
+bool is_draw_kernel_fn(const void *f);     // one of k_draw's / k_draw_sorted's host stubs
+bool is_sorted_draw_kernel_fn(const void *f);
 const void *lattice_draw_kernel_fn();      // k_lattice<true> (lattice + fused draw)
 hipError_t launch_prep(const tpe_hp *hps, int32_t n_hp, const double *mw,
                        const double *mmu, const double *msig, MixInfo *info,
@@ -200,6 +221,14 @@ hipError_t launch_lattice_draw(const ScoreArgs &a, const int32_t *hps_of_level, 
                                hipStream_t st);
 constexpr int kTabCap = 2048;  // below-mixture components of the LDS draw table
 hipError_t launch_draw(const ScoreArgs &a, bool table, hipStream_t st);
+// large draws: each block draws kSortedBlock consecutive candidates of a slot
+// and, for the per-candidate log-sum-exp / erf kinds, writes them grouped
+// into value buckets with their chunk positions in pos_out (tile coherence
+// for the log-sum-exp block skip and the erf dead-zone skip); small_table:
+// every below K <= kFuseTab
+constexpr int kSortedBlock = 2048;
+hipError_t launch_draw_sorted(const ScoreArgs &a, bool small_table, int32_t *pos_out,
+                              hipStream_t st);
 // slots slot_begin .. n_slots-1 (the lattice slots before them are not bucketed)
 hipError_t launch_bucket(const ScoreArgs &a, int32_t slot_begin, int32_t *pos_out, hipStream_t st);
 hipError_t launch_merge(const int32_t *level_hps, int32_t n_slots,

@@ -52,6 +52,122 @@ __global__ __launch_bounds__(kDrawThreads) void k_draw(ScoreArgs A) {
   }
 }
 
+// Large draws with value bucketing (the default above 4M draws): a block of
+// 256 threads draws kSortedBlock consecutive candidates of one (suggestion,
+// slot) -- 8 per thread -- and, for the per-candidate log-sum-exp and erf
+// kinds, writes them grouped into kSortBuckets equal-width value buckets of
+// the block's range (log scale for LGMM), with their chunk positions.  A
+// scoring tile (64 or 128 consecutive candidates) then spans a narrow value
+// range, so whole component blocks / chunks of a mixture are provably zero
+// for the wave and skipped (tpe_score.hip).  The candidate values are those
+// of the unsorted draw (counter = global index); only their order changes,
+// and the argmax tie-break uses the original index.
+constexpr int kSortBuckets = 128;
+
+// the scoring kind of a level slot: the groups are emitted heaviest kind
+// first (set_score_groups), not in slot order, so each group's slot range is
+// recovered from its block count
+__device__ __forceinline__ int slot_kind(const ScoreArgs &A, int slot) {
+  for (int g = 0; g < A.n_groups; ++g) {
+    const int nt = A.grp_tiles[g];
+    const int ns = nt > 0 ? (A.grp_block0[g + 1] - A.grp_block0[g]) / nt : 0;
+    if (slot >= A.grp_slot0[g] && slot < A.grp_slot0[g] + ns) return A.grp_kind[g];
+  }
+  return -1;
+}
+
+template <int CAP>
+struct SortedDrawLds {
+  DrawTableT<CAP> T;
+  double xs[kSortedBlock];          // the block's draws, in draw order
+  unsigned char bk[kSortedBlock];   // their buckets
+  int32_t hist[kSortBuckets];
+  double red[2][kDrawThreads / 64];
+};
+
+template <int CAP>
+__global__ __launch_bounds__(kDrawThreads) void k_draw_sorted(ScoreArgs A, int32_t *__restrict__ pos_out) {
+  __shared__ SortedDrawLds<CAP> L;
+  const int slot = blockIdx.y, s = blockIdx.z;
+  const int hp = A.level_hps[slot];
+  const tpe_hp H = A.hps[hp];
+  if (!hp_active(H, A.results + (int64_t)s * A.n_hp, A.cond_parent, A.cond_branch)) return;
+  const int64_t sb = 2 * (int64_t)hp;
+  const double *bw = A.mw + sb * A.kcap, *bmu = A.mmu + sb * A.kcap, *bsg = A.msig + sb * A.kcap;
+  const int K = A.info[sb].K;
+  const bool tab = K >= 1 && K <= CAP;
+  if (tab) build_table(H, K, bw, bmu, bsg, L.T);
+  const uint64_t seed = suggestion_seed(A, s);
+  const int64_t base = (int64_t)blockIdx.x * kSortedBlock;
+  const int n = (int)min<int64_t>(kSortedBlock, A.n_cand - base);
+  const int64_t off = (int64_t)s * A.cand_sstride + (int64_t)slot * A.n_cand + base;
+  double *out = const_cast<double *>(A.cand) + off;
+  const int t = threadIdx.x;
+  const int kind = slot_kind(A, slot);
+  const bool bucket = kind == KIND_LSE_G || kind == KIND_LSE_L || kind == KIND_LSE_G1 ||
+                      kind == KIND_LSE_L1 || kind == KIND_ERF_G || kind == KIND_ERF_L;
+  const bool lg = kind == KIND_LSE_L || kind == KIND_LSE_L1 || kind == KIND_ERF_L;
+  double lo = INFINITY, hi = -INFINITY;
+#pragma unroll 1
+  for (int i = t; i < n; i += kDrawThreads) {
+    const uint64_t gi = (uint64_t)(A.cand_begin + base + i);
+    const double x = tab ? draw_table_ool<CAP>(A.hps + hp, K, bmu, bsg, &L.T, seed, gi, (uint32_t)hp)
+                         : draw_one_ool(A.hps + hp, A.info + sb, bw, bmu, bsg, seed, gi, (uint32_t)hp);
+    if (!bucket) {
+      out[i] = x;
+      continue;
+    }
+    L.xs[i] = x;
+    const double key = lg ? log(x) : x;
+    if (fabs(key) < INFINITY) { lo = fmin(lo, key); hi = fmax(hi, key); }
+  }
+  if (!bucket) return;
+  // block range of the finite keys
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = fmin(lo, __shfl_xor(lo, o, 64));
+    hi = fmax(hi, __shfl_xor(hi, o, 64));
+  }
+  const int lane = t & 63, wv = t >> 6;
+  if (lane == 0) { L.red[0][wv] = lo; L.red[1][wv] = hi; }
+  for (int b = t; b < kSortBuckets; b += kDrawThreads) L.hist[b] = 0;
+  __syncthreads();
+  lo = INFINITY; hi = -INFINITY;
+#pragma unroll
+  for (int w = 0; w < kDrawThreads / 64; ++w) { lo = fmin(lo, L.red[0][w]); hi = fmax(hi, L.red[1][w]); }
+  const double scale = hi > lo ? (double)kSortBuckets / (hi - lo) : 0.0;
+  for (int i = t; i < n; i += kDrawThreads) {
+    const double x = L.xs[i];
+    const double key = lg ? log(x) : x;
+    int b = kSortBuckets - 1;
+    if (fabs(key) < INFINITY) b = min(kSortBuckets - 1, max(0, (int)((key - lo) * scale)));
+    L.bk[i] = (unsigned char)b;
+    atomicAdd(&L.hist[b], 1);
+  }
+  __syncthreads();
+  if (t < 64) {  // exclusive scan of the bucket counts, 2 per lane
+    static_assert(kSortBuckets == 128, "2 buckets per lane");
+    const int c0 = L.hist[2 * lane], c1 = L.hist[2 * lane + 1];
+    int v = c0 + c1;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int nb = __shfl_up(v, o, 64);
+      if (lane >= o) v += nb;
+    }
+    const int ex = v - (c0 + c1);
+    L.hist[2 * lane] = ex;
+    L.hist[2 * lane + 1] = ex + c0;
+  }
+  __syncthreads();
+  // scatter into the block's slice (16 KB + 8 KB, merged in L2)
+  int32_t *po = pos_out + off;
+  for (int i = t; i < n; i += kDrawThreads) {
+    const int p = atomicAdd(&L.hist[L.bk[i]], 1);
+    out[p] = L.xs[i];
+    po[p] = (int32_t)(base + i);
+  }
+}
+
 // Bucket each 8192-candidate chunk of the erf-kind hps by value (counting
 // sort into 256 equal-width buckets of the chunk's range, in the coordinate
 // the erf argument is linear in), keeping each candidate's original
@@ -286,7 +402,14 @@ hipError_t launch_micro(int which, int blocks, int iters, double *sink, hipStrea
 // ------------------------------------------------------------------------
 bool is_draw_kernel_fn(const void *f) {
   return f == reinterpret_cast<const void *>(&k_draw<true>) ||
-         f == reinterpret_cast<const void *>(&k_draw<false>);
+         f == reinterpret_cast<const void *>(&k_draw<false>) ||
+         f == reinterpret_cast<const void *>(&k_draw_sorted<kFuseTab>) ||
+         f == reinterpret_cast<const void *>(&k_draw_sorted<kTabCap>);
+}
+
+bool is_sorted_draw_kernel_fn(const void *f) {
+  return f == reinterpret_cast<const void *>(&k_draw_sorted<kFuseTab>) ||
+         f == reinterpret_cast<const void *>(&k_draw_sorted<kTabCap>);
 }
 
 hipError_t launch_draw(const ScoreArgs &a, bool table, hipStream_t st) {
@@ -297,6 +420,16 @@ hipError_t launch_draw(const ScoreArgs &a, bool table, hipStream_t st) {
   const unsigned gx = (unsigned)((a.n_cand + kDrawThreads * per - 1) / (kDrawThreads * per));
   if (table) k_draw<true><<<dim3(gx, a.n_slots, a.n_suggest), kDrawThreads, 0, st>>>(a);
   else k_draw<false><<<dim3(gx, a.n_slots, a.n_suggest), kDrawThreads, 0, st>>>(a);
+  return hipGetLastError();
+}
+
+hipError_t launch_draw_sorted(const ScoreArgs &a, bool small_table, int32_t *pos_out,
+                              hipStream_t st) {
+  if (a.n_slots <= 0 || a.n_suggest <= 0 || a.n_cand <= 0) return hipSuccess;
+  const unsigned gx = (unsigned)((a.n_cand + kSortedBlock - 1) / kSortedBlock);
+  const dim3 g(gx, a.n_slots, a.n_suggest);
+  if (small_table) k_draw_sorted<kFuseTab><<<g, kDrawThreads, 0, st>>>(a, pos_out);
+  else k_draw_sorted<kTabCap><<<g, kDrawThreads, 0, st>>>(a, pos_out);
   return hipGetLastError();
 }
 

@@ -4,26 +4,27 @@
 //   GMM1_lpdf   tpe.py:104-166     LGMM1_lpdf  tpe.py:259-301
 //   categorical_lpdf tpe.py:50-57  broadcast_best tpe.py:749-759 (EI argmax)
 //
-// Work decomposition.  A block of kWaves waves owns a tile of kTile = 64 * kR
+// Work decomposition.  A block of kWaves waves owns a tile of 64 * kR
 // candidates of one (suggestion, hp); every wave holds the same candidates,
 // kR per lane (candidate r * 64 + lane of the tile).  The components of both
-// mixtures are staged in LDS (batches of 1024, 32 KB) and wave w takes the
-// components with index = w (mod kWaves) of each mixture, reading each one by
-// broadcast once for its kR candidates, so a (candidate, component) pair costs
-// only VALU work, and the few live components of a quantized mixture (those
-// near the tile's value-sorted candidates) are spread over all waves.  Each
-// wave reduces its share per batch (log-sum-exp: a max pass and a sum pass;
-// quantized: a linear sum) and merges batches in order; then 2 * kR waves
-// (one per mixture and candidate row) merge the wave partials in wave order.
-// The reduction tree depends on (K_b, K_a) only, so scores are bitwise
+// mixtures are cut into chunks of kChunk; wave w takes the chunks w (mod
+// kWaves) and reads their coefficients with wave-uniform scalar loads (SGPR
+// operands: a (candidate, component) pair costs only VALU work, no LDS or
+// VGPR traffic).  Each wave reduces its share (log-sum-exp: single pass with
+// an integer exponent; quantized: a linear sum), then 2 * kR waves (one per
+// mixture and candidate row) merge the wave partials in wave order.  The
+// reduction tree depends on (K_b, K_a) only, so scores are bitwise
 // independent of the grid, of candidate chunking and of multi-GPU sharding.
 //
 // Log-sum-exp (q = None): t = alpha + y'(beta + gamma y') (two fp64 FMAs, see
-// make_coef), 2^(t - max) with v_exp_f32 on the fp64 difference, fp64
-// accumulation.  Quantized: the reference's sum_k w (Phi(ub) - Phi(lb)) in
-// fp64 with OCML erf, in its operation order; a component whose two erf
-// arguments are beyond 6.5 on one side contributes an exact 0 and is skipped
-// when every candidate of the wave agrees.
+// make_coef), 2^(t - m) with v_exp_f32 on the fp64 difference, fp32 group
+// sums added in fp64.  With value-bucketed candidates (large draws) a block
+// of 8 components whose envelope proves all its terms exact fp32 zeros for
+// the wave's candidates is skipped (lse_window / kLseDead): the sums are
+// bitwise those of the full loop.  Quantized: the reference's
+// sum_k w (Phi(ub) - Phi(lb)) in fp64 with OCML erf, in its operation order;
+// a component whose two erf arguments are beyond 6.5 on one side contributes
+// an exact 0 and is skipped when every candidate of the wave agrees.
 #include <math.h>
 
 #include <algorithm>
@@ -144,15 +145,44 @@ __device__ __forceinline__ void lse_group(const CoefGroup &g, int k, int nb,
   }
 }
 
-template <int KR>
+// The wave's pruning window for one mixture (lse_chunks' PRUNE mode): the
+// candidate range [lo, hi] (y' units) and the threshold below which a block's
+// bound proves every term an fp32 zero.
+struct LseWindow {
+  float lo, hi, thr;
+};
+
+// Census of the log-sum-exp work (roofline accounting only): valid pairs and
+// the ones in evaluated (not skipped) blocks.
+struct LseCensus {
+  uint32_t total, exec;
+};
+
+template <int KR, bool CENSUS>
 __device__ __forceinline__ void lse_chunks(KDbl *__restrict__ cs, int c0, int nb,
-                                           const double (&y)[KR], LseAcc (&out)[KR]) {
+                                           const double (&y)[KR], LseAcc (&out)[KR],
+                                           bool prune, LseWindow win, int nvalid,
+                                           LseCensus &cen) {
   double m[KR], s[KR];
 #pragma unroll
   for (int r = 0; r < KR; ++r) { m[r] = -INFINITY; s[r] = 0.0; }
   for (int c = c0; c * kChunk < nb; c += kWaves) {
     const int k1 = min(nb, (c + 1) * kChunk);
     for (int k = c * kChunk; k < k1; k += kGroup) {
+      if constexpr (CENSUS) cen.total += (uint32_t)(nvalid * min(kGroup, k1 - k));
+      if (prune) {
+        // the block envelope (4 floats in the w-row, one scalar load): skip
+        // the block when even its best term, anywhere in the wave's range,
+        // is below the lane maxima's lower bound by kLseDead -- an fp32
+        // exp2 of it is exactly 0, so the sums are unchanged
+        typedef const float __attribute__((address_space(4))) KFlt;
+        KFlt *e = reinterpret_cast<KFlt *>(cs + coef_off(k, 3));
+        const float elo = e[0], ehi = e[1], ec = e[2], ea = e[3];
+        const float d = fmaxf(0.0f, fmaxf(elo - win.hi, win.lo - ehi));
+        const float bound = fmaf(-ea, d * d, ec);
+        if (__builtin_amdgcn_readfirstlane((int)(bound < win.thr))) continue;
+      }
+      if constexpr (CENSUS) cen.exec += (uint32_t)(nvalid * min(kGroup, k1 - k));
       CoefGroup g;
       load_group(cs, k, g);
       if (k + kGroup <= k1) lse_group<KR, false>(g, k, k1, y, m, s);
@@ -165,6 +195,45 @@ __device__ __forceinline__ void lse_chunks(KDbl *__restrict__ cs, int c0, int nb
     else if (m[r] == -INFINITY) out[r] = s[r] == 0.0 ? LseAcc{-INFINITY, 0.0} : LseAcc{NAN, NAN};
     else out[r] = LseAcc{m[r], s[r]};
   }
+}
+
+// PRUNE setup: the wave's candidate range and, from the mixture's probe
+// component (its widest, the Parzen prior), a lower bound on every lane's
+// final exponent m (m >= max_k t_k >= t_probe).  Non-finite candidates or a
+// missing probe disable the skip (thr = -inf).
+template <int KR>
+__device__ __forceinline__ LseWindow lse_window(KDbl *__restrict__ cs, int probe, int K,
+                                                const double (&y)[KR], const bool (&valid)[KR]) {
+  double lo = INFINITY, hi = -INFINITY, tmin = INFINITY;
+  bool ok = probe >= 0 && probe < K;
+  const int p = ok ? probe : 0;
+  const double px = cs[coef_off(p, 0)], py = cs[coef_off(p, 1)], pz = cs[coef_off(p, 2)];
+#pragma unroll
+  for (int r = 0; r < KR; ++r) {
+    if (!valid[r]) continue;
+    ok &= fabs(y[r]) < INFINITY;
+    lo = fmin(lo, y[r]);
+    hi = fmax(hi, y[r]);
+    tmin = fmin(tmin, fma(fma(pz, y[r], py), y[r], px));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = fmin(lo, __shfl_xor(lo, o, 64));
+    hi = fmax(hi, __shfl_xor(hi, o, 64));
+    tmin = fmin(tmin, __shfl_xor(tmin, o, 64));
+  }
+  ok = __all(ok) && tmin == tmin && tmin > -1.0e30;
+  // fp32 window rounded outward, threshold one unit conservative; the
+  // (wave-uniform) values travel in SGPRs
+  const float flo = (float)lo, fhi = (float)hi;
+  float wl = ((double)flo > lo) ? nextafterf(flo, -INFINITY) : flo;
+  float wh = ((double)fhi < hi) ? nextafterf(fhi, INFINITY) : fhi;
+  float th = ok ? (float)(tmin - (double)kLseDead) - 1.0f : -INFINITY;
+  if (!(lo <= hi)) th = -INFINITY;  // no valid candidate in the wave
+  auto sf = [](float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
+  };
+  return LseWindow{sf(wl), sf(wh), sf(th)};
 }
 
 // CENSUS counts, per lane, the valid pairs, the live ones and the ones
@@ -344,8 +413,10 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
   const Coef *__restrict__ ca = A.coef + sa * A.kcap;
   const int64_t coff = (int64_t)s * A.cand_sstride + (int64_t)(A.cand_slot0 + slot) * A.n_cand;
   const double *__restrict__ cand = A.cand + coff;
-  // only the quantized kinds' candidates are value-bucketed (k_bucket)
-  const int32_t *__restrict__ cpos = (ERF && A.cand_pos) ? A.cand_pos + coff : nullptr;
+  // value-bucketed candidates (k_bucket, or the sorted draw) carry their
+  // chunk positions: the quantized kinds always, log-sum-exp when lse_pos
+  const int32_t *__restrict__ cpos =
+      ((ERF || (LSE && A.lse_pos)) && A.cand_pos) ? A.cand_pos + coff : nullptr;
 
   int64_t li[KR];
   bool valid[KR];
@@ -407,12 +478,19 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
     // wave index as a scalar: the component addresses below are wave-uniform,
     // so the coefficients come in through scalar loads (SGPR operands)
     const int wv = __builtin_amdgcn_readfirstlane(wave);
+    LseCensus lcen{0u, 0u};
+    int nvalid = 0;
+#pragma unroll
+    for (int r = 0; r < KR; ++r) nvalid += valid[r] ? 1 : 0;
 #pragma unroll
     for (int mix = 0; mix < 2; ++mix) {
       const Coef *__restrict__ cm = mix ? ca : cb;
       const int K = mix ? ia.K : ib.K;
       if constexpr (LSE) {
-        lse_chunks<KR>(uniform_ptr(cm), wv, K, y, lacc[mix]);
+        const bool prune = A.lse_prune != 0;
+        LseWindow win{0.0f, 0.0f, -INFINITY};
+        if (prune) win = lse_window<KR>(uniform_ptr(cm), mix ? ia.probe : ib.probe, K, y, valid);
+        lse_chunks<KR, CENSUS>(uniform_ptr(cm), wv, K, y, lacc[mix], prune, win, nvalid, lcen);
       } else {
         erf_chunks<KR, LOGN, CENSUS>(uniform_ptr(cm), wv, K, ub, lb, valid, wlo, whi, exact, pacc[mix], cen);
       }
@@ -425,6 +503,19 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) c3[q] += __shfl_xor(c3[q], o, 64);
         if (lane == 0) atomicAdd(A.census + q, c3[q]);
+      }
+    }
+    if constexpr (CENSUS && LSE) {
+      // nvalid is per lane: the per-lane sums add up to the wave's pairs
+      unsigned long long c2[2] = {lcen.total, lcen.exec};
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) c2[q] += __shfl_xor(c2[q], o, 64);
+      }
+      if (lane == 0) {
+        atomicAdd(A.census + 3, c2[0]);
+        atomicAdd(A.census + 5, c2[1]);
       }
     }
 #pragma unroll
@@ -739,7 +830,8 @@ hipError_t launch_score(const ScoreArgs &a, bool has_erf, hipStream_t st) {
     if (a.census) k_score<true, true><<<g, kWaves * 64, 0, st>>>(a);
     else k_score<true, false><<<g, kWaves * 64, 0, st>>>(a);
   } else {
-    k_score<false, false><<<g, kWaves * 64, 0, st>>>(a);
+    if (a.census) k_score<false, true><<<g, kWaves * 64, 0, st>>>(a);
+    else k_score<false, false><<<g, kWaves * 64, 0, st>>>(a);
   }
   return hipGetLastError();
 }

@@ -241,11 +241,19 @@ int tpe_plan_profile_read(tpe_plan_t p, int32_t kind, double *avg_ms,
 int tpe_plan_set_lattice(tpe_plan_t p, int32_t enable);
 
 /* Roofline accounting: read (counts may be NULL) and clear the census of the
- * quantized-kind scoring work since the last call -- counts[0] valid
- * (candidate, component) pairs, [1] live pairs (not an exact zero), [2]
- * pairs evaluated (live for some lane of their wave) -- and switch the
- * census on (enable != 0) or off for the following suggests.               */
+ * scoring work since the last call -- counts[0] valid quantized (candidate,
+ * component) pairs, [1] live ones (not an exact zero), [2] quantized pairs
+ * evaluated (live for some lane of their wave), [3] valid log-sum-exp pairs,
+ * [4] reserved (0), [5] log-sum-exp pairs evaluated (outside the component
+ * blocks skipped as exact zeros) -- and switch the census on (enable != 0)
+ * or off for the following suggests.  counts has 6 entries.               */
 int tpe_plan_census(tpe_plan_t p, int32_t enable, int64_t *counts);
+
+/* Large draws score log-sum-exp candidates on value-bucketed tiles and skip
+ * the blocks of 8 mixture components whose terms are exact fp32 zeros for
+ * every candidate of a wave (bitwise the same sums).  enable = 0 evaluates
+ * every (candidate, component) pair, for A/B measurement and tests.       */
+int tpe_plan_set_prune(tpe_plan_t p, int32_t enable);
 
 /* Register-only microbenchmarks for the roofline: which = 0 v_exp_f32
  * (results/s), 1 fp64 FMA (flop/s), 2 OCML fp64 erf (results/s), 3 the

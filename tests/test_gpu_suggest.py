@@ -406,3 +406,34 @@ def test_thread_trials_async_batched_tpe():
     assert len(t) == 120
     assert all(d['state'] == H.JOB_STATE_DONE for d in t.trials)
     assert min(t.losses()) < 1e-2
+
+
+@pytest.mark.parametrize('name', ['cfg2', 'cond'])
+def test_pruned_lse_bitwise_equals_full_evaluation(name):
+    """Large draws (>= 4M candidate draws) are value-bucketed by the draw and
+    log-sum-exp tiles skip the component blocks whose terms are exact fp32
+    zeros: every record (score bits included) equals the unpruned run, and
+    equals the merge of two differently-tiled shards in index and value."""
+    torch = pytest.importorskip('torch')
+    meta, d, dom, trials = _fixture_trials(name)
+    tpe.suggest([meta['new_id']], dom, trials, 7, n_EI_candidates=64)
+    plan = dom._tpe_state.plan
+    n = 1 << 18 if name == 'cfg2' else 1 << 20
+    plan.set_prune(True)
+    plan.census(True)
+    got = plan.suggest([21, 22], n)
+    c = plan.census(False)
+    plan.set_prune(False)
+    want = plan.suggest([21, 22], n)
+    plan.set_prune(True)
+    np.testing.assert_array_equal(got.view(np.uint8), want.view(np.uint8))
+    assert c[3] > 0 and c[5] < c[3], c          # blocks were skipped
+    if name != 'cfg2':
+        return                                   # one level: shards merge directly
+    cut = 77_777
+    parts = [plan.suggest([21], cut, cand_begin=0), plan.suggest([21], n - cut, cand_begin=cut)]
+    raw = torch.from_numpy(np.stack(parts).view(np.uint8).reshape(-1).copy()).cuda()
+    merged = plan.merge(raw.data_ptr(), world=2, level=0)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(merged[0]['index'], got[0]['index'])
+    np.testing.assert_array_equal(merged[0]['value'], got[0]['value'])
