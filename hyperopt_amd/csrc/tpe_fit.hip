@@ -679,9 +679,13 @@ __device__ void prep_slot(const tpe_hp &H, int64_t slot, int K, const double *w,
   const bool quant = (H.flags & TPE_HAS_Q) != 0;
   for (int k = threadIdx.x; k < K; k += blockDim.x)
     store_coef(cf, k, make_coef(H, w[k], mu[k], sg[k], pacc), quant);
-  if (!quant)
+  if (!quant) {
     for (int b = threadIdx.x; b * kCoefBlock < K; b += blockDim.x)
       store_lse_envelope(H, cf, b, K, w, mu, sg, pacc);
+    // padding of the last block: terms 2^-inf = 0 (the scoring loop has no tail mask)
+    for (int k = K + (int)threadIdx.x; k < (K + kCoefBlock - 1) / kCoefBlock * kCoefBlock; k += blockDim.x)
+      store_coef(cf, k, Coef{-INFINITY, 0.0, 0.0, 0.0}, false);
+  }
   if (threadIdx.x == 0) {
     MixInfo mi;
     mi.K = K; mi.kind = quant ? 1 : 0; mi.p_accept = pacc; mi.log_pacc = log(pacc);
@@ -786,9 +790,13 @@ __device__ void fit_continuous(const FitArgs &A, const FitCtx &C, FitShared &sm,
     store_coef(cf, k, make_coef(H, wk, mk, s, pacc), quant);
     if (MIXLDS) { gw[k] = wk; gm[k] = mk; gs[k] = s; }
   }
-  if (!quant)
+  if (!quant) {
     for (int b = threadIdx.x; b * kCoefBlock < K; b += blockDim.x)
       store_lse_envelope(H, cf, b, K, w, mu, sg, pacc);
+    // padding of the last block: terms 2^-inf = 0 (the scoring loop has no tail mask)
+    for (int k = K + (int)threadIdx.x; k < (K + kCoefBlock - 1) / kCoefBlock * kCoefBlock; k += blockDim.x)
+      store_coef(cf, k, Coef{-INFINITY, 0.0, 0.0, 0.0}, false);
+  }
   if (threadIdx.x == 0) {
     MixInfo mi;
     mi.K = K; mi.kind = quant ? 1 : 0; mi.p_accept = pacc; mi.log_pacc = log(pacc);

@@ -158,35 +158,69 @@ struct LseCensus {
   uint32_t total, exec;
 };
 
+// A block's envelope bound over the wave's candidate range [lo, hi]: the
+// largest term any of its components can reach there (log2 units).
+__device__ __forceinline__ float envelope_bound(const float4 e, const LseWindow &win) {
+  const float d = fmaxf(0.0f, fmaxf(e.x - win.hi, win.lo - e.y));
+  return fmaf(-e.w, d * d, e.z);
+}
+
+// The wave's chunks c = c0 (mod kWaves) of a mixture of nb components, in
+// increasing order, 64 chunks per round: lane l first tests the two blocks
+// of chunk c0 + kWaves * (64 r + l) against the window (one vector load of
+// their envelopes, tpe_internal.hpp kLseDead), a ballot gives the round's
+// live blocks, and only those are evaluated -- in the same order as the
+// full loop, so the sums are bitwise those of evaluating every block
+// (skipped terms are exact fp32 zeros).  prune = false: every block is live.
 template <int KR, bool CENSUS>
-__device__ __forceinline__ void lse_chunks(KDbl *__restrict__ cs, int c0, int nb,
-                                           const double (&y)[KR], LseAcc (&out)[KR],
-                                           bool prune, LseWindow win, int nvalid,
-                                           LseCensus &cen) {
+__device__ __forceinline__ void lse_chunks(KDbl *__restrict__ cs, const Coef *__restrict__ cv,
+                                           int c0, int nb, const double (&y)[KR],
+                                           LseAcc (&out)[KR], bool prune, LseWindow win,
+                                           int nvalid, LseCensus &cen) {
+  const int lane = threadIdx.x & 63;
   double m[KR], s[KR];
 #pragma unroll
   for (int r = 0; r < KR; ++r) { m[r] = -INFINITY; s[r] = 0.0; }
-  for (int c = c0; c * kChunk < nb; c += kWaves) {
-    const int k1 = min(nb, (c + 1) * kChunk);
-    for (int k = c * kChunk; k < k1; k += kGroup) {
-      if constexpr (CENSUS) cen.total += (uint32_t)(nvalid * min(kGroup, k1 - k));
-      if (prune) {
-        // the block envelope (4 floats in the w-row, one scalar load): skip
-        // the block when even its best term, anywhere in the wave's range,
-        // is below the lane maxima's lower bound by kLseDead -- an fp32
-        // exp2 of it is exactly 0, so the sums are unchanged
-        typedef const float __attribute__((address_space(4))) KFlt;
-        KFlt *e = reinterpret_cast<KFlt *>(cs + coef_off(k, 3));
-        const float elo = e[0], ehi = e[1], ec = e[2], ea = e[3];
-        const float d = fmaxf(0.0f, fmaxf(elo - win.hi, win.lo - ehi));
-        const float bound = fmaf(-ea, d * d, ec);
-        if (__builtin_amdgcn_readfirstlane((int)(bound < win.thr))) continue;
+  const int nch = (nb + kChunk - 1) / kChunk;
+  for (int r0 = c0; r0 < nch; r0 += kWaves * 64) {
+    const int c = r0 + kWaves * lane;
+    const int k0 = c * kChunk;
+    const bool has0 = c < nch, has1 = has0 && k0 + kGroup < nb;
+    bool live0 = has0, live1 = has1;
+    if (prune && has0) {
+      const double *t = reinterpret_cast<const double *>(cv);
+      const float4 e0 = *reinterpret_cast<const float4 *>(t + coef_off(k0, 3));
+      live0 = envelope_bound(e0, win) >= win.thr;
+      if (has1) {
+        const float4 e1 = *reinterpret_cast<const float4 *>(t + coef_off(k0 + kGroup, 3));
+        live1 = envelope_bound(e1, win) >= win.thr;
       }
-      if constexpr (CENSUS) cen.exec += (uint32_t)(nvalid * min(kGroup, k1 - k));
-      CoefGroup g;
-      load_group(cs, k, g);
-      if (k + kGroup <= k1) lse_group<KR, false>(g, k, k1, y, m, s);
-      else lse_group<KR, true>(g, k, k1, y, m, s);
+    }
+    if constexpr (CENSUS) {
+      const int n0 = has0 ? min(kGroup, nb - k0) : 0, n1 = has1 ? min(kGroup, nb - k0 - kGroup) : 0;
+      uint32_t tot = (uint32_t)(n0 + n1), ex = (uint32_t)((live0 ? n0 : 0) + (live1 ? n1 : 0));
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        tot += __shfl_xor(tot, o, 64);
+        ex += __shfl_xor(ex, o, 64);
+      }
+      cen.total += tot * (uint32_t)nvalid;
+      cen.exec += ex * (uint32_t)nvalid;
+    }
+    uint64_t m0 = __ballot(live0), m1 = __ballot(live1);
+    // live blocks in order: chunk j's block 0 before its block 1 before chunk
+    // j + 1 (the padding components of a last block have alpha = -inf,
+    // make_coef_pad, so no tail masking is needed)
+    while (m0 | m1) {
+      const int j0 = m0 ? __builtin_ctzll(m0) : 64, j1 = m1 ? __builtin_ctzll(m1) : 64;
+      const int g = j1 < j0 ? 1 : 0;
+      const int j = g ? j1 : j0;
+      if (g) m1 &= m1 - 1;
+      else m0 &= m0 - 1;
+      const int kg = (r0 + kWaves * j) * kChunk + g * kGroup;
+      CoefGroup cgp;
+      load_group(cs, kg, cgp);
+      lse_group<KR, false>(cgp, kg, nb, y, m, s);
     }
   }
 #pragma unroll
@@ -490,7 +524,8 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
         const bool prune = A.lse_prune != 0;
         LseWindow win{0.0f, 0.0f, -INFINITY};
         if (prune) win = lse_window<KR>(uniform_ptr(cm), mix ? ia.probe : ib.probe, K, y, valid);
-        lse_chunks<KR, CENSUS>(uniform_ptr(cm), wv, K, y, lacc[mix], prune, win, nvalid, lcen);
+        lse_chunks<KR, CENSUS>(uniform_ptr(cm), cm, wv, K, y, lacc[mix], prune, win, nvalid,
+                               lcen);
       } else {
         erf_chunks<KR, LOGN, CENSUS>(uniform_ptr(cm), wv, K, ub, lb, valid, wlo, whi, exact, pacc[mix], cen);
       }

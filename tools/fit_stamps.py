@@ -23,7 +23,7 @@ def main(cfg, slots):
     import torch
     torch.cuda.set_device(0)
     eng = E.Engine(0)
-    dom, losses, vals, active, _ = bench.build_workload(cfg)
+    dom, losses, vals, active = bench.build_workload(cfg)
     hps, conds, pprior = dom.space.engine_tables()
     plan = E.Plan(eng, hps, conds, pprior, max_trials=losses.size)
     plan.set_history(losses, vals, active)

@@ -16,7 +16,7 @@ def main(cfgs):
     eng = E.Engine(0)
     st = torch.cuda.Stream()
     for cfg in cfgs:
-        dom, losses, vals, active, _ = bench.build_workload(cfg)
+        dom, losses, vals, active = bench.build_workload(cfg)
         hps, conds, pprior = dom.space.engine_tables()
         plan = E.Plan(eng, hps, conds, pprior, max_trials=losses.size)
         plan.set_history(losses, vals, active)

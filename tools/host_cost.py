@@ -18,7 +18,8 @@ def main(n=200):
     torch.cuda.set_device(0)
     from hyperopt_amd import _engine as E
     eng = E.Engine(0)
-    dom, losses, vals, active, n_cand = bench.build_workload('cfg2')
+    dom, losses, vals, active = bench.build_workload('cfg2')
+    n_cand = bench.CONFIGS['cfg2']['n_cand']
     hps, conds, pprior = dom.space.engine_tables()
     plan = E.Plan(eng, hps, conds, pprior, max_trials=losses.size)
     plan.set_history(losses, vals, active)

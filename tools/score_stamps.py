@@ -27,7 +27,8 @@ def main(cfg, n_cand):
         dom, losses, vals, active = kind_bench.workload(cfg[5:])
         nc = 4096
     else:
-        dom, losses, vals, active, nc = bench.build_workload(cfg)
+        dom, losses, vals, active = bench.build_workload(cfg)
+        nc = bench.CONFIGS[cfg]['n_cand']
     n_cand = n_cand or nc
     hps, conds, pprior = dom.space.engine_tables()
     plan = E.Plan(eng, hps, conds, pprior, max_trials=losses.size)
