@@ -57,8 +57,11 @@ struct MixInfo {
 // so t_k(y') <= c_max - a2_min * dist(y', [mu'_lo, mu'_hi])^2 for every
 // component k of the block.  The scoring kernel skips a block whose bound,
 // over the wave's candidate range, is below (lower bound of the lane maxima)
-// - kLseDead: its terms are exact zeros of the fp32 exp2.
-constexpr float kLseDead = 151.0f;
+// - kLseDead - 1: each skipped term is < 2^-65 of the lane's largest term
+// (>= 1/2 of the sum), so a mixture of K components moves the lpdf by at
+// most K * 2^-64 relative (5e-16 at K = 1e4) -- fp64 rounding level, 1e9
+// times inside the 1e-6 parity bar.
+constexpr float kLseDead = 64.0f;
 // census counters (tpe_plan_census): quantized total / live / evaluated,
 // log-sum-exp total / (reserved) / evaluated
 constexpr int kCensus = 6;
@@ -226,7 +229,7 @@ hipError_t launch_draw(const ScoreArgs &a, bool table, hipStream_t st);
 // into value buckets with their chunk positions in pos_out (tile coherence
 // for the log-sum-exp block skip and the erf dead-zone skip); small_table:
 // every below K <= kFuseTab
-constexpr int kSortedBlock = 2048;
+constexpr int kSortedBlock = 4096;
 hipError_t launch_draw_sorted(const ScoreArgs &a, bool small_table, int32_t *pos_out,
                               hipStream_t st);
 // slots slot_begin .. n_slots-1 (the lattice slots before them are not bucketed)

@@ -54,7 +54,7 @@ __global__ __launch_bounds__(kDrawThreads) void k_draw(ScoreArgs A) {
 
 // Large draws with value bucketing (the default above 4M draws): a block of
 // 256 threads draws kSortedBlock consecutive candidates of one (suggestion,
-// slot) -- 8 per thread -- and, for the per-candidate log-sum-exp and erf
+// slot) -- 16 per thread -- and, for the per-candidate log-sum-exp and erf
 // kinds, writes them grouped into kSortBuckets equal-width value buckets of
 // the block's range (log scale for LGMM), with their chunk positions.  A
 // scoring tile (64 or 128 consecutive candidates) then spans a narrow value
@@ -62,7 +62,7 @@ __global__ __launch_bounds__(kDrawThreads) void k_draw(ScoreArgs A) {
 // for the wave and skipped (tpe_score.hip).  The candidate values are those
 // of the unsorted draw (counter = global index); only their order changes,
 // and the argmax tie-break uses the original index.
-constexpr int kSortBuckets = 128;
+constexpr int kSortBuckets = 256;
 
 // the scoring kind of a level slot: the groups are emitted heaviest kind
 // first (set_score_groups), not in slot order, so each group's slot range is
@@ -145,21 +145,23 @@ __global__ __launch_bounds__(kDrawThreads) void k_draw_sorted(ScoreArgs A, int32
     atomicAdd(&L.hist[b], 1);
   }
   __syncthreads();
-  if (t < 64) {  // exclusive scan of the bucket counts, 2 per lane
-    static_assert(kSortBuckets == 128, "2 buckets per lane");
-    const int c0 = L.hist[2 * lane], c1 = L.hist[2 * lane + 1];
-    int v = c0 + c1;
+  if (t < 64) {  // exclusive scan of the bucket counts, 4 per lane
+    static_assert(kSortBuckets == 256, "4 buckets per lane");
+    int c[4], tot = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { c[j] = L.hist[4 * lane + j]; tot += c[j]; }
+    int v = tot;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const int nb = __shfl_up(v, o, 64);
       if (lane >= o) v += nb;
     }
-    const int ex = v - (c0 + c1);
-    L.hist[2 * lane] = ex;
-    L.hist[2 * lane + 1] = ex + c0;
+    int acc = v - tot;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { L.hist[4 * lane + j] = acc; acc += c[j]; }
   }
   __syncthreads();
-  // scatter into the block's slice (16 KB + 8 KB, merged in L2)
+  // scatter into the block's slice (32 KB + 16 KB, merged in L2)
   int32_t *po = pos_out + off;
   for (int i = t; i < n; i += kDrawThreads) {
     const int p = atomicAdd(&L.hist[L.bk[i]], 1);

@@ -19,9 +19,10 @@
 // Log-sum-exp (q = None): t = alpha + y'(beta + gamma y') (two fp64 FMAs, see
 // make_coef), 2^(t - m) with v_exp_f32 on the fp64 difference, fp32 group
 // sums added in fp64.  With value-bucketed candidates (large draws) a block
-// of 8 components whose envelope proves all its terms exact fp32 zeros for
-// the wave's candidates is skipped (lse_window / kLseDead): the sums are
-// bitwise those of the full loop.  Quantized: the reference's
+// of 8 components whose envelope proves all its terms below 2^-65 of every
+// lane's largest term is skipped (lse_window / kLseDead): the lpdf moves by
+// at most K * 2^-64 relative, and only with the candidate's own components
+// (a skip never depends on how the candidates are tiled beyond that bound).  Quantized: the reference's
 // sum_k w (Phi(ub) - Phi(lb)) in fp64 with OCML erf, in its operation order;
 // a component whose two erf arguments are beyond 6.5 on one side contributes
 // an exact 0 and is skipped when every candidate of the wave agrees.
@@ -169,9 +170,8 @@ __device__ __forceinline__ float envelope_bound(const float4 e, const LseWindow 
 // increasing order, 64 chunks per round: lane l first tests the two blocks
 // of chunk c0 + kWaves * (64 r + l) against the window (one vector load of
 // their envelopes, tpe_internal.hpp kLseDead), a ballot gives the round's
-// live blocks, and only those are evaluated -- in the same order as the
-// full loop, so the sums are bitwise those of evaluating every block
-// (skipped terms are exact fp32 zeros).  prune = false: every block is live.
+// live blocks, and only those are evaluated, in the same order as the full
+// loop.  prune = false: every block is live.
 template <int KR, bool CENSUS>
 __device__ __forceinline__ void lse_chunks(KDbl *__restrict__ cs, const Coef *__restrict__ cv,
                                            int c0, int nb, const double (&y)[KR],
