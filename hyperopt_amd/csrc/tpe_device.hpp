@@ -117,7 +117,7 @@ __device__ __forceinline__ Coef make_coef(const tpe_hp &H, double w, double mu, 
 
 // The log-sum-exp envelope of coefficient block b (components [8b, 8b+8) of
 // K) of a continuous mixture, written into the block's w-row as 4 floats
-// (tpe_internal.hpp, kLseDead).  Same c and a^2 as make_coef.
+// (tpe_internal.hpp, kLseDeadBase).  Same c and a^2 as make_coef.
 __device__ __forceinline__ void store_lse_envelope(const tpe_hp &H, Coef *table, int b, int K,
                                                    const double *w, const double *mu,
                                                    const double *sg, double pacc) {

@@ -57,11 +57,11 @@ struct MixInfo {
 // so t_k(y') <= c_max - a2_min * dist(y', [mu'_lo, mu'_hi])^2 for every
 // component k of the block.  The scoring kernel skips a block whose bound,
 // over the wave's candidate range, is below (lower bound of the lane maxima)
-// - kLseDead - 1: each skipped term is < 2^-65 of the lane's largest term
-// (>= 1/2 of the sum), so a mixture of K components moves the lpdf by at
-// most K * 2^-64 relative (5e-16 at K = 1e4) -- fp64 rounding level, 1e9
-// times inside the 1e-6 parity bar.
-constexpr float kLseDead = 64.0f;
+// - D - 1 with D = kLseDeadBase + ceil(log2 K): each skipped term is below
+// 2^-(D+1) of the lane's largest term (>= 1/2 of the sum), so all skipped
+// terms of a K-component mixture move the lpdf by at most K * 2^-D <=
+// 2^-kLseDeadBase ~ 1e-9 relative -- 1000x inside the 1e-6 parity bar.
+constexpr float kLseDeadBase = 30.0f;
 // census counters (tpe_plan_census): quantized total / live / evaluated,
 // log-sum-exp total / (reserved) / evaluated
 constexpr int kCensus = 6;

@@ -19,10 +19,9 @@
 // Log-sum-exp (q = None): t = alpha + y'(beta + gamma y') (two fp64 FMAs, see
 // make_coef), 2^(t - m) with v_exp_f32 on the fp64 difference, fp32 group
 // sums added in fp64.  With value-bucketed candidates (large draws) a block
-// of 8 components whose envelope proves all its terms below 2^-65 of every
-// lane's largest term is skipped (lse_window / kLseDead): the lpdf moves by
-// at most K * 2^-64 relative, and only with the candidate's own components
-// (a skip never depends on how the candidates are tiled beyond that bound).  Quantized: the reference's
+// of 8 components whose envelope proves all its terms below 2^-(31 + log2 K)
+// of every lane's largest term is skipped (lse_window, kLseDeadBase): the
+// lpdf moves by at most 2^-30 ~ 1e-9 relative.  Quantized: the reference's
 // sum_k w (Phi(ub) - Phi(lb)) in fp64 with OCML erf, in its operation order;
 // a component whose two erf arguments are beyond 6.5 on one side contributes
 // an exact 0 and is skipped when every candidate of the wave agrees.
@@ -169,7 +168,7 @@ __device__ __forceinline__ float envelope_bound(const float4 e, const LseWindow 
 // The wave's chunks c = c0 (mod kWaves) of a mixture of nb components, in
 // increasing order, 64 chunks per round: lane l first tests the two blocks
 // of chunk c0 + kWaves * (64 r + l) against the window (one vector load of
-// their envelopes, tpe_internal.hpp kLseDead), a ballot gives the round's
+// their envelopes, tpe_internal.hpp kLseDeadBase), a ballot gives the round's
 // live blocks, and only those are evaluated, in the same order as the full
 // loop.  prune = false: every block is live.
 template <int KR, bool CENSUS>
@@ -262,7 +261,8 @@ __device__ __forceinline__ LseWindow lse_window(KDbl *__restrict__ cs, int probe
   const float flo = (float)lo, fhi = (float)hi;
   float wl = ((double)flo > lo) ? nextafterf(flo, -INFINITY) : flo;
   float wh = ((double)fhi < hi) ? nextafterf(fhi, INFINITY) : fhi;
-  float th = ok ? (float)(tmin - (double)kLseDead) - 1.0f : -INFINITY;
+  const float dead = kLseDeadBase + (float)(32 - __builtin_clz((unsigned)max(K - 1, 1)));
+  float th = ok ? (float)(tmin - (double)dead) - 1.0f : -INFINITY;
   if (!(lo <= hi)) th = -INFINITY;  // no valid candidate in the wave
   auto sf = [](float v) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));

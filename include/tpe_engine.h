@@ -250,8 +250,9 @@ int tpe_plan_set_lattice(tpe_plan_t p, int32_t enable);
 int tpe_plan_census(tpe_plan_t p, int32_t enable, int64_t *counts);
 
 /* Large draws score log-sum-exp candidates on value-bucketed tiles and skip
- * the blocks of 8 mixture components whose every term is below 2^-65 of
- * each candidate's largest one (lpdf moved by <= K * 2^-64 relative).
+ * the blocks of 8 mixture components whose every term is below
+ * 2^-(31 + log2 K) of each candidate's largest one (lpdf moved by <= 2^-30
+ * ~ 1e-9 relative).
  * enable = 0 evaluates every (candidate, component) pair, for A/B
  * measurement and tests.                                                   */
 int tpe_plan_set_prune(tpe_plan_t p, int32_t enable);

@@ -412,8 +412,8 @@ def test_thread_trials_async_batched_tpe():
 def test_pruned_lse_equals_full_evaluation(name):
     """Large draws (>= 4M candidate draws) are value-bucketed by the draw and
     log-sum-exp tiles skip the component blocks whose terms are all below
-    2^-65 of every candidate's largest: winners (index, value) equal the
-    unpruned run and scores agree within K * 2^-64 relative (1e-12 here);
+    2^-(31 + log2 K) of every candidate's largest: winners (index, value)
+    equal the unpruned run and scores agree within 2^-30 relative per lpdf;
     the winner also equals the merge of two differently tiled shards."""
     torch = pytest.importorskip('torch')
     meta, d, dom, trials = _fixture_trials(name)
@@ -430,7 +430,7 @@ def test_pruned_lse_equals_full_evaluation(name):
     np.testing.assert_array_equal(got['index'], want['index'])
     np.testing.assert_array_equal(got['value'], want['value'])
     np.testing.assert_array_equal(got['active'], want['active'])
-    np.testing.assert_allclose(got['score'], want['score'], rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(got['score'], want['score'], rtol=4e-9, atol=4e-9)
     assert c[3] > 0 and c[5] < c[3], c          # blocks were skipped
     if name != 'cfg2':
         return                                   # one level: shards merge directly

@@ -12,9 +12,9 @@ O=gpurun_out/$cfg
 mkdir -p "$O"
 timeout -k 10 400 python -u bench.py --config "$cfg" "$@" > "$O/bench.json" 2> "$O/bench.err"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$O/trace" -o run -- \
-    python -u bench.py --config "$cfg" "$@" --no-cpu-baseline > "$O/trace.log" 2>&1
+    python -u bench.py --config "$cfg" "$@" --no-cpu-baseline --no-e2e > "$O/trace.log" 2>&1
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$O/fetch" -o run -- \
-    python -u bench.py --config "$cfg" "$@" --no-cpu-baseline > "$O/fetch.log" 2>&1
+    python -u bench.py --config "$cfg" "$@" --no-cpu-baseline --no-e2e > "$O/fetch.log" 2>&1
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d "$O/write" -o run -- \
-    python -u bench.py --config "$cfg" "$@" --no-cpu-baseline > "$O/write.log" 2>&1
+    python -u bench.py --config "$cfg" "$@" --no-cpu-baseline --no-e2e > "$O/write.log" 2>&1
 echo "done $cfg"

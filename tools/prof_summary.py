@@ -23,8 +23,8 @@ KIND = {0: 'lse_gmm', 1: 'lse_lgmm', 2: 'erf_gmm', 3: 'erf_lgmm', 4: 'categorica
 
 
 def short(name):
-    if 'k_score' in name:   # k_score<erf, census>: the census and per-candidate
-        if 'k_score<true, true>' in name:      # erf variants are bench A/B passes
+    if 'k_score' in name:   # k_score<erf, census>: the census variants run in
+        if ', true>' in name:                  # the bench's separate census pass
             return 'k_score_census'
         return 'k_score_erf' if 'k_score<true, false>' in name else 'k_score'
     m = re.search(r'(k_\w+(?:<\d>)?)', name)
