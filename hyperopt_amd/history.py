@@ -253,3 +253,4 @@ class TrialHistory(object):
         plan._history_owner = self
         self._dev = weakref.ref(plan)
         self._vals_dirty = self._loss_dirty = self.n
+        return self
