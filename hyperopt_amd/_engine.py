@@ -40,6 +40,7 @@ EXPORTS = (
     'tpe_plan_profile', 'tpe_plan_profile_read', 'tpe_microbench', 'tpe_plan_get_results',
     'tpe_plan_results_device', 'tpe_plan_census', 'tpe_plan_fit_suggest',
     'tpe_plan_set_lattice', 'tpe_plan_update_history', 'tpe_plan_set_prune',
+    'tpe_plan_sample_prior',
 )
 
 
@@ -146,6 +147,7 @@ def load_library(path: str = LIB_PATH):
             'tpe_plan_census': (C.c_int, [vp, i32, C.POINTER(i64)]),
             'tpe_plan_set_lattice': (C.c_int, [vp, i32]),
             'tpe_plan_set_prune': (C.c_int, [vp, i32]),
+            'tpe_plan_sample_prior': (C.c_int, [vp, C.POINTER(u64), i64, vp, i32, vp]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -437,6 +439,18 @@ class Plan(object):
                 optr, 0 if host else 1, stream))
         self._last_nsug = seeds.size
         self._last_ncand = int(n_cand)
+        return res
+
+    def sample_prior(self, seeds, stream=None):
+        """Prior draws of len(seeds) whole suggestions (rand.suggest on the
+        device): [S, n_hp] RESULT_DTYPE, value/active per hp."""
+        e = self.engine
+        seeds = _seeds(seeds)
+        res = np.empty((seeds.size, self.n_hp), dtype=RESULT_DTYPE)
+        with e.lock:
+            e.check(e.lib.tpe_plan_sample_prior(self.p, seeds.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                                seeds.size, res.ctypes.data, 0, stream))
+        self._last_nsug = seeds.size
         return res
 
     def results(self):

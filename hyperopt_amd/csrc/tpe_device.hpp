@@ -85,8 +85,14 @@ __device__ __forceinline__ bool hp_active(const tpe_hp &H, const Partial *res,
 //   Centring keeps alpha, beta y' and gamma y'^2 within ~(100 |mu'| / range)^2 of
 //   t, i.e. cancellation costs < 1e-12 absolute in fp64.
 //  ERF (q given): (mu, 1 / max(sqrt(2) sigma, EPS), w) for the CDF differences.
+// The log-sum-exp envelope contribution of one component (its mu', c, a^2);
+// neutral values for padding components.
+struct EnvTerm {
+  double m, c, a2;
+};
+
 __device__ __forceinline__ Coef make_coef(const tpe_hp &H, double w, double mu, double sigma,
-                                          double pacc) {
+                                          double pacc, EnvTerm *env = nullptr) {
 #pragma clang fp contract(off)
   Coef c;
   c.w = 0.0;
@@ -112,42 +118,36 @@ __device__ __forceinline__ Coef make_coef(const tpe_hp &H, double w, double mu, 
   c.x = cc - a2 * (m * m);                     // alpha
   c.y = 2.0 * a2 * m;                          // beta
   c.z = -a2;                                   // gamma
+  if (env) *env = EnvTerm{m, cc, a2};
   return c;
 }
 
-// The log-sum-exp envelope of coefficient block b (components [8b, 8b+8) of
-// K) of a continuous mixture, written into the block's w-row as 4 floats
-// (tpe_internal.hpp, kLseDeadBase).  Same c and a^2 as make_coef.
-__device__ __forceinline__ void store_lse_envelope(const tpe_hp &H, Coef *table, int b, int K,
-                                                   const double *w, const double *mu,
-                                                   const double *sg, double pacc) {
-#pragma clang fp contract(off)
-  const double L2E = 1.4426950408889634;
-  double lo = INFINITY, hi = -INFINITY, cmax = -INFINITY, amin = INFINITY;
-  for (int k = b * kCoefBlock; k < min(K, (b + 1) * kCoefBlock); ++k) {
-    const double sp = np_maximum(sg[k], kEPS);
-    double cc;
-    if (H.family == TPE_GMM) {
-      const double Z = sqrt(2.0 * 3.141592653589793 * (sg[k] * sg[k]));
-      cc = L2E * log(w[k] / Z / pacc);
-    } else {
-      cc = L2E * (log(w[k]) - log(sp * 2.5066282746310002));
-    }
-    const double a2 = (0.5 * L2E) / (sp * sp);
-    const double m = mu[k] - H.prior_mu;
-    lo = fmin(lo, m);
-    hi = fmax(hi, m);
-    cmax = (cc == cc) ? fmax(cmax, cc) : INFINITY;  // a NaN term: never skip
-    amin = fmin(amin, a2);
+// The block envelope of the 8 consecutive components held by the 8 lanes
+// (lane & 7) of this lane's group: reduced with xor shuffles (all 8 lanes
+// must be active), written by the group's first lane into the block's w-row
+// as 4 floats rounded outward (tpe_internal.hpp, kLseDeadBase).  NaN terms
+// disable the skip of the block.
+__device__ __forceinline__ void store_lse_envelope(Coef *table, int64_t k, EnvTerm e, bool valid) {
+  // padding lanes (valid = false) contribute the neutral element
+  double lo = valid ? e.m : INFINITY, hi = valid ? e.m : -INFINITY;
+  double cm = !valid ? -INFINITY : (e.c == e.c) ? e.c : INFINITY, am = valid ? e.a2 : INFINITY;
+  bool bad = valid && (!(e.m == e.m) || !(e.a2 == e.a2));
+#pragma unroll
+  for (int o = 1; o < kCoefBlock; o <<= 1) {
+    lo = fmin(lo, __shfl_xor(lo, o, 64));
+    hi = fmax(hi, __shfl_xor(hi, o, 64));
+    cm = fmax(cm, __shfl_xor(cm, o, 64));
+    am = fmin(am, __shfl_xor(am, o, 64));
+    bad |= __shfl_xor((int)bad, o, 64) != 0;
   }
-  // outward fp32 rounding: the float box contains the exact one
-  float *e = reinterpret_cast<float *>(reinterpret_cast<double *>(table) + coef_off(b * kCoefBlock, 3));
-  const float flo = (float)lo, fhi = (float)hi, fc = (float)cmax, fa = (float)amin;
-  e[0] = ((double)flo > lo) ? nextafterf(flo, -INFINITY) : flo;
-  e[1] = ((double)fhi < hi) ? nextafterf(fhi, INFINITY) : fhi;
-  e[2] = ((double)fc < cmax) ? nextafterf(fc, INFINITY) : fc;
-  e[3] = ((double)fa > amin) ? nextafterf(fa, 0.0f) : fa;
-  if (!(amin == amin) || !(lo == lo) || !(hi == hi)) { e[2] = INFINITY; e[3] = 0.0f; }
+  if (k % kCoefBlock) return;
+  float *out = reinterpret_cast<float *>(reinterpret_cast<double *>(table) + coef_off(k, 3));
+  const float flo = (float)lo, fhi = (float)hi, fc = (float)cm, fa = (float)am;
+  out[0] = ((double)flo > lo) ? nextafterf(flo, -INFINITY) : flo;
+  out[1] = ((double)fhi < hi) ? nextafterf(fhi, INFINITY) : fhi;
+  out[2] = ((double)fc < cm) ? nextafterf(fc, INFINITY) : fc;
+  out[3] = ((double)fa > am) ? nextafterf(fa, 0.0f) : fa;
+  if (bad) { out[2] = INFINITY; out[3] = 0.0f; }
 }
 
 }  // namespace tpe

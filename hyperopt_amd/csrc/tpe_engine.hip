@@ -46,6 +46,7 @@ struct tpe_plan {
   // device buffers
   tpe_hp *d_hps = nullptr;
   int32_t *d_cp = nullptr, *d_cb = nullptr, *d_level_hps = nullptr, *d_all_hps = nullptr;
+  int32_t *d_level_off = nullptr;  // level_off on the device (k_prior)
   double *d_pprior = nullptr;
   double *d_losses = nullptr, *d_vals = nullptr;
   uint8_t *d_active = nullptr, *d_below = nullptr;
@@ -161,6 +162,7 @@ hipStream_t pick_stream(tpe_engine *h, void *s) {
 
 void plan_free_buffers(tpe_plan *p) {
   void *bufs[] = {p->d_hps, p->d_cp, p->d_cb, p->d_level_hps, p->d_all_hps, p->d_pprior,
+                  p->d_level_off,
                   p->d_losses, p->d_vals, p->d_active, p->d_below, p->d_mw, p->d_mmu,
                   p->d_msig, p->d_scratch, p->d_info, p->d_coef, p->d_results, p->d_seeds,
                   p->d_partial, p->d_ext, p->d_lb, p->d_la, p->d_cand, p->d_cpos,
@@ -323,6 +325,7 @@ int plan_build(tpe_engine *h, const tpe_space *sp, int64_t max_trials, tpe_plan 
   CKH(dalloc(&p->d_pprior, p->pprior.size()));
   CKH(dalloc(&p->d_level_hps, p->P));
   CKH(dalloc(&p->d_all_hps, p->P));
+  CKH(dalloc(&p->d_level_off, p->level_off.size()));
   CKH(dalloc(&p->d_losses, p->ncap));
   CKH(dalloc(&p->d_vals, (size_t)p->ncap * p->P));
   CKH(dalloc(&p->d_active, (size_t)p->ncap * p->P));
@@ -357,6 +360,8 @@ int plan_build(tpe_engine *h, const tpe_space *sp, int64_t max_trials, tpe_plan 
     CKH(hipMemcpyAsync(p->d_pprior, p->pprior.data(), p->pprior.size() * 8, hipMemcpyHostToDevice, st));
   CKH(hipMemcpyAsync(p->d_level_hps, lh.data(), lh.size() * 4, hipMemcpyHostToDevice, st));
   CKH(hipMemcpyAsync(p->d_all_hps, all.data(), all.size() * 4, hipMemcpyHostToDevice, st));
+  CKH(hipMemcpyAsync(p->d_level_off, p->level_off.data(), p->level_off.size() * 4,
+                     hipMemcpyHostToDevice, st));
   CKH(hipMemsetAsync(p->d_info, 0, slots * sizeof(MixInfo), st));
   CKH(hipStreamSynchronize(st));
   return TPE_OK;
@@ -1443,6 +1448,38 @@ int tpe_plan_census(tpe_plan_t p, int32_t enable, int64_t *counts) {
   CKH(hipMemset(p->d_census, 0, kCensus * sizeof(unsigned long long)));
   p->census = enable != 0;
   return TPE_OK;
+}
+
+int tpe_plan_sample_prior(tpe_plan_t p, const uint64_t *seeds, int64_t n_sug, tpe_result *out,
+                          int32_t out_on_device, void *stream) {
+  if (!p) return TPE_E_INVALID;
+  tpe_engine *h = p->eng;
+  if (n_sug <= 0 || !seeds) return fail(h, TPE_E_INVALID, "bad args");
+  CKH(hipSetDevice(h->device));
+  hipStream_t st = pick_stream(h, stream);
+  int rc = ensure_suggest_state(h, p, n_sug, 1);
+  if (rc) return rc;
+  CKH(hipMemcpyAsync(p->d_seeds, seeds, n_sug * 8, hipMemcpyHostToDevice, st));
+  PriorArgs a{};
+  a.hps = p->d_hps;
+  a.n_hp = p->P;
+  a.n_levels = (int32_t)p->levels.size();
+  a.level_hps = p->d_level_hps;
+  a.level_off = p->d_level_off;
+  a.cond_parent = p->d_cp;
+  a.cond_branch = p->d_cb;
+  a.pprior = p->d_pprior;
+  a.seeds = p->d_seeds;
+  a.results = p->d_results;
+  CKH(launch_prior(a, (int32_t)n_sug, st));
+  p->last_nsug = n_sug;
+  if (!out_on_device) {
+    // the host seeds buffer must outlive the async copy: synchronize here
+    rc = copy_results(h, p, n_sug, out, 0, st);
+    if (rc) return rc;
+    return TPE_OK;
+  }
+  return copy_results(h, p, n_sug, out, out_on_device, st);
 }
 
 int tpe_plan_set_prune(tpe_plan_t p, int32_t enable) {

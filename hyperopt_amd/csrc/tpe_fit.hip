@@ -644,6 +644,27 @@ __device__ Split compute_split(const FitArgs &A, const FitCtx &C, FitShared &sm)
 }
 
 // ------------------------------------------------------------------------
+// the scoring table of a continuous slot (block-wide): coefficients of the K
+// components, and for log-sum-exp kinds the block envelopes (one xor-shuffle
+// reduction per 8 components, computed with the coefficients) and the
+// padding components of the last block (alpha = -inf: terms exactly 0).
+// ------------------------------------------------------------------------
+__device__ void store_table(const tpe_hp &H, Coef *cf, int K, const double *w, const double *mu,
+                            const double *sg, double pacc, bool quant) {
+  const int kp = (K + kCoefBlock - 1) / kCoefBlock * kCoefBlock;
+  // kp and the block size are multiples of 8: the 8 lanes of a block's
+  // components are active together for the shuffles
+  for (int k = threadIdx.x; k < (quant ? K : kp); k += blockDim.x) {
+    EnvTerm e{0.0, 0.0, 0.0};
+    const bool real = k < K;
+    const Coef c = real ? make_coef(H, w[k], mu[k], sg[k], pacc, &e)
+                        : Coef{-INFINITY, 0.0, 0.0, 0.0};
+    store_coef(cf, k, c, quant);
+    if (!quant) store_lse_envelope(cf, k, e, real);
+  }
+}
+
+// ------------------------------------------------------------------------
 // per-component lpdf constants + truncation mass of one slot (block-wide);
 // w/mu/sg may be LDS or global; tmp: K doubles of scratch
 // ------------------------------------------------------------------------
@@ -677,15 +698,7 @@ __device__ void prep_slot(const tpe_hp &H, int64_t slot, int K, const double *w,
   }
   STAMP(8);
   const bool quant = (H.flags & TPE_HAS_Q) != 0;
-  for (int k = threadIdx.x; k < K; k += blockDim.x)
-    store_coef(cf, k, make_coef(H, w[k], mu[k], sg[k], pacc), quant);
-  if (!quant) {
-    for (int b = threadIdx.x; b * kCoefBlock < K; b += blockDim.x)
-      store_lse_envelope(H, cf, b, K, w, mu, sg, pacc);
-    // padding of the last block: terms 2^-inf = 0 (the scoring loop has no tail mask)
-    for (int k = K + (int)threadIdx.x; k < (K + kCoefBlock - 1) / kCoefBlock * kCoefBlock; k += blockDim.x)
-      store_coef(cf, k, Coef{-INFINITY, 0.0, 0.0, 0.0}, false);
-  }
+  store_table(H, cf, K, w, mu, sg, pacc, quant);
   if (threadIdx.x == 0) {
     MixInfo mi;
     mi.K = K; mi.kind = quant ? 1 : 0; mi.p_accept = pacc; mi.log_pacc = log(pacc);
@@ -785,18 +798,9 @@ __device__ void fit_continuous(const FitArgs &A, const FitCtx &C, FitShared &sm,
   // per-component lpdf constants (tpe.py:138-160, 277-299) + copy-out
   const bool quant = (H.flags & TPE_HAS_Q) != 0;
   Coef *cf = A.coef + slot * A.kcap;
-  for (int k = threadIdx.x; k < K; k += blockDim.x) {
-    const double s = sg[k], wk = w[k], mk = mu[k];
-    store_coef(cf, k, make_coef(H, wk, mk, s, pacc), quant);
-    if (MIXLDS) { gw[k] = wk; gm[k] = mk; gs[k] = s; }
-  }
-  if (!quant) {
-    for (int b = threadIdx.x; b * kCoefBlock < K; b += blockDim.x)
-      store_lse_envelope(H, cf, b, K, w, mu, sg, pacc);
-    // padding of the last block: terms 2^-inf = 0 (the scoring loop has no tail mask)
-    for (int k = K + (int)threadIdx.x; k < (K + kCoefBlock - 1) / kCoefBlock * kCoefBlock; k += blockDim.x)
-      store_coef(cf, k, Coef{-INFINITY, 0.0, 0.0, 0.0}, false);
-  }
+  if (MIXLDS)
+    for (int k = threadIdx.x; k < K; k += blockDim.x) { gw[k] = w[k]; gm[k] = mu[k]; gs[k] = sg[k]; }
+  store_table(H, cf, K, w, mu, sg, pacc, quant);
   if (threadIdx.x == 0) {
     MixInfo mi;
     mi.K = K; mi.kind = quant ? 1 : 0; mi.p_accept = pacc; mi.log_pacc = log(pacc);

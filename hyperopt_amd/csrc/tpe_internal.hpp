@@ -246,4 +246,20 @@ hipError_t launch_sample(const tpe_hp *hp_dev, const double *mw,
 
 hipError_t launch_micro(int which, int blocks, int iters, double *sink, hipStream_t st);
 
+// prior draws of whole suggestions (rand.suggest on the device): one block
+// per suggestion walks the levels of the compiled space
+struct PriorArgs {
+  const tpe_hp *hps;
+  int32_t n_hp;
+  int32_t n_levels;
+  const int32_t *level_hps;   // hp ids, level by level
+  const int32_t *level_off;   // [n_levels + 1] (device)
+  const int32_t *cond_parent;
+  const int32_t *cond_branch;
+  const double *pprior;
+  const uint64_t *seeds;      // [S]
+  Partial *results;           // [S][P]
+};
+hipError_t launch_prior(const PriorArgs &a, int32_t n_suggest, hipStream_t st);
+
 }  // namespace tpe

@@ -293,6 +293,70 @@ __global__ __launch_bounds__(256) void k_sample(const tpe_hp *__restrict__ hpd,
 }
 
 // ------------------------------------------------------------------------
+// Prior draws (rand.suggest, hyperopt/rand.py:14-33, and the samplers of
+// pyll/stochastic.py:30-142): every active hp of a suggestion drawn from its
+// prior -- uniform / loguniform / quniform / qloguniform (the descriptor's
+// bounds, log-space for LGMM), normal / lognormal / qnormal / qlognormal
+// (prior_mu, prior_sigma), randint / choice (uniform index) and pchoice (the
+// prior p).  One block per suggestion; a level's activity reads the values
+// its parents drew (vectorize.py:20-38 routing).  Counter-based Philox keyed
+// by the suggestion seed, stream = hp | 2^31 (disjoint from candidate draws).
+// ------------------------------------------------------------------------
+__device__ double prior_value(const tpe_hp &H, const double *pprior, uint64_t seed, int hp) {
+  const Draw d = draw4(seed, 0, 0x80000000u | (uint32_t)hp, 0);
+  if (H.family == TPE_CAT) {
+    if (H.flags & TPE_PCHOICE) {            // stochastic.py:104-142: multinomial on p
+      const double *p = pprior + H.pprior_begin;
+      double tot = 0.0;
+      for (int c = 0; c < H.upper; ++c) tot += p[c];
+      const double t = d.u0 * tot;
+      double acc = 0.0;
+      for (int c = 0; c < H.upper - 1; ++c) {
+        acc += p[c];
+        if (t < acc) return (double)c;
+      }
+      return (double)(H.upper - 1);
+    }
+    return fmin(floor(d.u0 * (double)H.upper), (double)(H.upper - 1));   // randint
+  }
+  double x;
+  if (H.flags & (TPE_HAS_LOW | TPE_HAS_HIGH)) {
+    x = H.low + d.u0 * (H.high - H.low);    // uniform on [low, high)
+    if (!(x < H.high)) x = nextafter(H.high, -INFINITY);
+  } else {                                  // normal(mu, sigma), Box-Muller
+    x = H.prior_mu + H.prior_sigma * (sqrt(-2.0 * log(1.0 - d.u1)) * cospi(2.0 * d.u2));
+  }
+  if (H.family == TPE_LGMM) x = exp(x);
+  if (H.flags & TPE_HAS_Q) x = rint(x / H.q) * H.q;
+  return x;
+}
+
+__global__ __launch_bounds__(256) void k_prior(PriorArgs A) {
+  const int s = blockIdx.x;
+  const uint64_t seed = A.seeds[s];
+  Partial *res = A.results + (int64_t)s * A.n_hp;
+  for (int l = 0; l < A.n_levels; ++l) {
+    const int b = A.level_off[l], e = A.level_off[l + 1];
+    for (int i = b + (int)threadIdx.x; i < e; i += blockDim.x) {
+      const int hp = A.level_hps[i];
+      const tpe_hp H = A.hps[hp];
+      if (!hp_active(H, res, A.cond_parent, A.cond_branch)) {
+        res[hp] = Partial{NAN, NAN, -1, 0, 0};
+        continue;
+      }
+      res[hp] = Partial{0.0, prior_value(H, A.pprior, seed, hp), 0, 1, 0};
+    }
+    __syncthreads();  // the next level reads its parents' draws
+  }
+}
+
+hipError_t launch_prior(const PriorArgs &a, int32_t n_suggest, hipStream_t st) {
+  if (n_suggest <= 0 || a.n_hp <= 0) return hipSuccess;
+  k_prior<<<n_suggest, 256, 0, st>>>(a);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------
 // register-only microkernels for the roofline (tpe_microbench)
 // ------------------------------------------------------------------------
 template <int WHICH>

@@ -1,7 +1,10 @@
 """Random search / TPE startup (hyperopt/rand.py).
 
-Host-side prior sampling with the reference's RandomState stream, so the
-first ``n_startup_jobs`` trials of a TPE run are identical to the reference's.
+``rng_stream='numpy'`` (default): host-side prior sampling with the
+reference's RandomState stream, so random search and the first
+``n_startup_jobs`` trials of a TPE run are identical to the reference's.
+``rng_stream='philox'``: the same priors drawn on the device
+(``tpe_plan_sample_prior``), all ids of the call in one launch.
 """
 from __future__ import annotations
 
@@ -15,8 +18,12 @@ def _value(h, v):
     return int(v) if h.is_categorical else v
 
 
-def suggest(new_ids, domain, trials, seed):
+def suggest(new_ids, domain, trials, seed, rng_stream='numpy'):
     """hyperopt/rand.py:14-33: one pass over the space per new id."""
+    if rng_stream == 'philox':
+        return _suggest_device(new_ids, domain, trials, seed)
+    if rng_stream != 'numpy':
+        raise ValueError('rng_stream must be "numpy" or "philox"')
     cs = domain.space
     rng = np.random.RandomState(seed)
     rval = []
@@ -53,3 +60,22 @@ def suggest_batch(new_ids, domain, trials, seed):
             idxs[lab].append(i)
             vals[lab].append(v)
     return idxs, vals
+
+
+def _suggest_device(new_ids, domain, trials, seed):
+    """Prior draws on the GPU: suggestion i keyed by tpe.batch_seeds(seed)[i]."""
+    from . import tpe
+    new_ids = list(new_ids)
+    if not new_ids:
+        return []
+    cs = domain.space
+    st = tpe._state(domain)
+    with st.lock:
+        plan = st.plan_for(domain, 1, tpe.E.default_engine())
+        res = plan.sample_prior(tpe.batch_seeds(seed, len(new_ids)))
+    out = []
+    for s, new_id in enumerate(new_ids):
+        chosen = {h.label: _value(h, float(res[s, h.index]['value']))
+                  for h in cs.hps if res[s, h.index]['active']}
+        out.append(tpe._new_doc(domain, trials, cs, new_id, chosen))
+    return out

@@ -132,10 +132,13 @@ def suggest(new_ids, domain, trials, seed,
             n_EI_candidates=_default_n_EI_candidates,
             gamma=_default_gamma,
             linear_forgetting=_default_linear_forgetting,
-            rng_stream='philox', engine=None):
+            rng_stream='philox', startup_stream='numpy', engine=None):
     """hyperopt/tpe.py:804-897 on the GPU, one document per id in
     ``new_ids``.  ``linear_forgetting`` is accepted and, as in the reference
-    (tpe.py:809), not used: LF is fixed at 25."""
+    (tpe.py:809), not used: LF is fixed at 25.  The first ``n_startup_jobs``
+    trials come from ``rand.suggest`` with ``startup_stream``: 'numpy' (the
+    reference's RandomState stream, default) or 'philox' (device prior
+    draws, tpe_plan_sample_prior)."""
     new_ids = list(new_ids)
     if not new_ids:
         return []
@@ -145,8 +148,12 @@ def suggest(new_ids, domain, trials, seed,
     st = _state(domain)
     with st.lock:
         hist = st.history(domain, trials).sync(trials)
-        if hist.n < n_startup_jobs:
-            return rand.suggest(new_ids, domain, trials, seed)
+        startup = hist.n < n_startup_jobs
+    if startup:
+        # the reference's RandomState prior stream (numpy), or device prior
+        # draws with the Philox stream (tpe_plan_sample_prior)
+        return rand.suggest(new_ids, domain, trials, seed, rng_stream=startup_stream)
+    with st.lock:
         engine = engine or E.default_engine()
         plan = st.plan_for(domain, hist.n, engine)
         hist.push(plan)

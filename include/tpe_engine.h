@@ -249,6 +249,15 @@ int tpe_plan_set_lattice(tpe_plan_t p, int32_t enable);
  * or off for the following suggests.  counts has 6 entries.               */
 int tpe_plan_census(tpe_plan_t p, int32_t enable, int64_t *counts);
 
+/* Prior draws of n_suggest whole suggestions (rand.suggest, the TPE startup
+ * phase: hyperopt/rand.py:14-33, pyll/stochastic.py:30-142): every active hp
+ * drawn from its prior, conditional hps routed by their parents' draws;
+ * results[s][hp] = (0, value, 0, active=1) or (NaN, NaN, -1, 0) inactive.
+ * Counter-based Philox keyed by seeds[s] (stream disjoint from candidate
+ * draws); the history is not read.                                          */
+int tpe_plan_sample_prior(tpe_plan_t p, const uint64_t *seeds, int64_t n_suggest,
+                          tpe_result *out, int32_t out_on_device, void *stream);
+
 /* Large draws score log-sum-exp candidates on value-bucketed tiles and skip
  * the blocks of 8 mixture components whose every term is below
  * 2^-(31 + log2 K) of each candidate's largest one (lpdf moved by <= 2^-30
