@@ -229,3 +229,42 @@ def test_categorical_posterior_sizes(eng, n, upper):
     pp = rng.dirichlet(np.ones(upper))
     p = eng.categorical_posterior(obs, upper, 0.5, pp)
     np.testing.assert_array_equal(p, O.categorical_posterior(obs, upper, 0.5, pp))
+
+
+@pytest.mark.parametrize('q,bounds', [(1, (None, None)), (2, (None, None)), (0.5, (None, None)),
+                                      (0.125, (None, None)), (1, (2, 4)), (2, (2, 4)),
+                                      (1, (1, 4.1)), (2, (1, 4.1))])
+def test_qlgmm_sampler_matches_lpdf(eng, q, bounds):
+    """hyperopt/tests/test_tpe.py:424-514 (TestQLGMM1Math) on the device
+    sampler: quantized log-GMM draws are multiples of q, inside the
+    (log-space) bounds, and their lattice frequencies fit exp(LGMM1_lpdf) --
+    chi-square over 20000 draws (lattice points with >= 20 expected hits,
+    the rest pooled), plus the reference's own error bounds on the first 20
+    lattice points of 1001 draws."""
+    from scipy.stats import chisquare
+    from hyperopt_amd._engine import LGMM
+    w, mu, sg = [.1, .3, .4, .2], [-2.0, 0.0, -3.0, 1.0], [2.1, .4, .8, 2.1]
+    low, high = bounds
+    for n, seed in ((20000, 11), (1001, 234)):
+        s = eng.sample(LGMM, w, mu, sg, low=low, high=high, q=q, seed=seed, n=n) / q
+        assert np.all(s == s.astype(int))
+        if low is not None:
+            assert s.min() * q >= np.round(np.exp(low) / q) * q - 1e-12
+            assert s.max() * q <= np.round(np.exp(high) / q) * q + 1e-12
+        lo, hi = int(s.min()), int(s.max())
+        counts = np.bincount(s.astype(int) - lo)
+        xc = np.arange(lo, hi + 1) * q
+        with np.errstate(divide='ignore'):
+            prob = np.exp(O.lgmm_lpdf(xc, w, mu, sg, low=low, high=high, q=q))
+        if n == 1001:
+            err = ((prob - counts / float(n)) ** 2)[:20]
+            assert np.max(err) < .1 and np.mean(err) < .01 and np.median(err) < .01
+            continue
+        exp = prob * n
+        big = exp >= 20
+        obs_b, exp_b = counts[big], exp[big]
+        rest_o, rest_e = n - obs_b.sum(), n - exp_b.sum()
+        if rest_e >= 20:
+            obs_b, exp_b = np.append(obs_b, rest_o), np.append(exp_b, rest_e)
+        exp_b = exp_b * obs_b.sum() / exp_b.sum()
+        assert chisquare(obs_b, exp_b).pvalue > 1e-4, (q, bounds)
