@@ -215,12 +215,34 @@ def e2e_latency(cfg, n_calls):
 
 
 # ----------------------------------------------------------------------------
-def _launch_ranks(n):
-    """Re-launch under torch.distributed.run (child process; no GPU touched yet)."""
+class _StdoutToStderr(object):
+    """fd-level redirect of stdout to stderr (RCCL prints its version banner
+    on stdout when a communicator comes up; the bench's stdout is one JSON
+    line)."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+        return self
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+        return False
+
+
+def _free_port():
     import socket
     with socket.socket() as s:
         s.bind(('127.0.0.1', 0))
-        port = s.getsockname()[1]
+        return s.getsockname()[1]
+
+
+def _launch_ranks(n):
+    """Re-launch under torch.distributed.run (child process; no GPU touched yet)."""
+    port = _free_port()
     cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
            '--nproc-per-node=%d' % n, '--master-addr=127.0.0.1', '--master-port=%d' % port,
            os.path.abspath(__file__)] + sys.argv[1:]
@@ -240,6 +262,9 @@ def main():
     ap.add_argument('--cpu-seconds', type=float, default=10.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-e2e', action='store_true')
+    ap.add_argument('--parallelism', default='auto', choices=['auto', 'single', 'sharded'],
+                    help="auto: the config's multi-GPU mode when N > 1; 'sharded' forces the "
+                         "candidate-sharded path (RCCL all-gather + device merge) even at N = 1")
     ap.add_argument('--traffic-json', default=os.path.join(ROOT, 'profiles', 'traffic.json'))
     args = ap.parse_args()
 
@@ -261,10 +286,18 @@ def main():
 
     import torch
     torch.cuda.set_device(local)
+    if args.parallelism == 'sharded':
+        C = dict(C, mode='sharded')
     dist = None
-    if world > 1:
+    if world > 1 or args.parallelism == 'sharded':
         import torch.distributed as dist
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if 'MASTER_ADDR' not in os.environ:     # a one-rank group for --parallelism sharded
+            os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(_free_port()),
+                              RANK='0', WORLD_SIZE='1')
+        with _StdoutToStderr():
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+            dist.barrier()          # brings the communicator up (and its banner)
+            torch.cuda.synchronize()
 
     from hyperopt_amd import _engine as E
     from hyperopt_amd import parallel, tpe
@@ -280,7 +313,7 @@ def main():
     plan.set_history_device(d_losses.data_ptr(), d_vals.data_ptr(), d_act.data_ptr(),
                             losses.size)
 
-    mode = C['mode'] if world > 1 else 'single'
+    mode = C['mode'] if (world > 1 or args.parallelism == 'sharded') else 'single'
     sharded = parallel.ShardedSuggest(plan) if mode == 'sharded' else None
     if args.config == 'cfg5':
         mine = list(parallel.suggestion_slice(C['batch'], rank, world))

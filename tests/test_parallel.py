@@ -171,3 +171,87 @@ def test_sharded_suggest_two_ranks_equals_single_device():
             np.testing.assert_array_equal(got['active'], full['active'])
             np.testing.assert_array_equal(got['index'], full['index'])
             np.testing.assert_array_equal(got['value'], full['value'])
+
+
+def _gpu_worker_cfg4(rank, world, port, outdir, n_cand):
+    """Config 4 (100-D, N = 1e4, K_a ~ 9976) sharded over the ranks, as
+    bench.py --config cfg4 --gpus N runs it (bucketed draws, block skip)."""
+    import torch
+    import torch.distributed as dist
+    from hyperopt_amd import hp, _engine as E
+    from hyperopt_amd.base import Domain
+    import big_configs
+    _init(rank, world, port)
+    torch.cuda.set_device(0)
+    dom, losses, vals, act = big_configs.cfg4_domain_history(hp, Domain)
+    hps, conds, pprior = dom.space.engine_tables()
+    plan = E.Plan(E.Engine(0), hps, conds, pprior, max_trials=losses.size)
+    plan.set_history(losses, vals, act)
+    plan.fit()
+    sharded = PAR.ShardedSuggest(plan).suggest([7], n_cand)
+    if rank == 0:
+        full = plan.suggest([7], n_cand)
+        np.save(os.path.join(outdir, 'full.npy'), full.view(np.uint8))
+    np.save(os.path.join(outdir, 'r%d.npy' % rank), sharded.view(np.uint8))
+    torch.cuda.synchronize()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_sharded_config4_two_ranks_equals_single_device():
+    """bench.py's multi-GPU config-4 mode on one GPU with two ranks: the
+    all-gathered, device-merged winners of every hp equal one device's
+    (index and value; scores within the block-skip bound)."""
+    import torch.multiprocessing as mp
+    port = _free_port()
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_gpu_worker_cfg4, args=(2, port, d, 1 << 22), nprocs=2, join=True)
+        full = np.load(os.path.join(d, 'full.npy')).view(RESULT_DTYPE)
+        assert (full['active'] == 1).all() and (full['index'] >= 0).all()
+        for r in range(2):
+            got = np.load(os.path.join(d, 'r%d.npy' % r)).view(RESULT_DTYPE)
+            np.testing.assert_array_equal(got['index'], full['index'])
+            np.testing.assert_array_equal(got['value'], full['value'])
+            np.testing.assert_allclose(got['score'], full['score'], rtol=4e-9, atol=4e-9)
+
+
+def _nccl_worker(rank, world, port, outdir):
+    """One rank over RCCL (backend 'nccl'): ShardedSuggest's gather takes the
+    all_gather_into_tensor branch on device memory."""
+    import torch
+    import torch.distributed as dist
+    import hyperopt_amd as H
+    from hyperopt_amd import hp, rand, Trials, trials_from_docs, _engine as E
+    from hyperopt_amd.base import Domain
+    from hyperopt_amd.tpe import build_history
+    import spaces
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group('nccl', rank=rank, world_size=world,
+                            device_id=torch.device('cuda', 0))
+    dom = Domain(lambda x: 0.0, spaces.cond_space(hp))
+    docs = rand.suggest(list(range(300)), dom, Trials(), 3)
+    for d, l in zip(docs, np.random.RandomState(4).rand(300)):
+        d['state'] = H.JOB_STATE_DONE
+        d['result'] = {'status': 'ok', 'loss': float(l)}
+    _, losses, vals, act = build_history(dom, trials_from_docs(docs), dom.space.labels)
+    hps, conds, pprior = dom.space.engine_tables()
+    plan = E.Plan(E.Engine(0), hps, conds, pprior, max_trials=losses.size)
+    plan.set_history(losses, vals, act)
+    plan.fit()
+    assert dist.get_backend() == 'nccl'
+    got = PAR.ShardedSuggest(plan).suggest([5, 6], 3000)
+    full = plan.suggest([5, 6], 3000)
+    np.save(os.path.join(outdir, 'got.npy'), got.view(np.uint8))
+    np.save(os.path.join(outdir, 'full.npy'), full.view(np.uint8))
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_sharded_suggest_over_rccl_one_rank():
+    import torch.multiprocessing as mp
+    port = _free_port()
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_nccl_worker, args=(1, port, d), nprocs=1, join=True)
+        got = np.load(os.path.join(d, 'got.npy'))
+        np.testing.assert_array_equal(got, np.load(os.path.join(d, 'full.npy')))
