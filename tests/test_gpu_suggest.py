@@ -441,3 +441,37 @@ def test_pruned_lse_equals_full_evaluation(name):
     torch.cuda.synchronize()
     np.testing.assert_array_equal(merged[0]['index'], got[0]['index'])
     np.testing.assert_array_equal(merged[0]['value'], got[0]['value'])
+
+
+def test_graph_replay_across_fused_draw_threshold():
+    """a graph captured while n_below + 1 <= 32 (lattice launch
+    carrying the draw rows, 32-entry tables) must not be replayed once n_below
+    reaches 32 (gamma_cap = 64): the step key includes the fused-draw choice.
+    Child process with TPE_GRAPH=1; every call equals eager fit + suggest."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path.insert(0, 'tests'); import test_gpu_suggest as t; "
+            "t._graph_threshold_body(); print('OK')")
+    r = subprocess.run([sys.executable, '-c', code], cwd=root, env=dict(os.environ, TPE_GRAPH='1'),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and 'OK' in r.stdout, (r.stdout[-1000:], r.stderr[-3000:])
+
+
+def _graph_threshold_body():
+    meta, d, dom, trials = _fixture_trials('cfg2')
+    tpe.suggest([meta['new_id']], dom, trials, 7, n_EI_candidates=64)
+    plan = dom._tpe_state.plan
+    from hyperopt_amd.tpe import build_history
+    _, losses, vals, active = build_history(dom, trials, dom.space.labels)
+    # n_below = min(ceil(0.25 sqrt(n)), 64): 500 -> 6, 16000 would be 32;
+    # with gamma 1.0: n = 900 -> 30 (fused), n = 1000 -> 32 (not fused)
+    for i, (m, seed) in enumerate([(900, 3), (900, 4), (900, 5), (1000, 6), (1000, 7),
+                                   (900, 8), (1000, 9)]):
+        plan.set_history(losses[:m], vals[:, :m], active[:, :m])
+        got = plan.fit_suggest([seed], 512, gamma=1.0, gamma_cap=64)
+        plan.fit(gamma=1.0, gamma_cap=64)
+        want = plan.suggest([seed], 512)
+        assert np.isfinite(got['value'][got['active'] == 1]).all(), i
+        np.testing.assert_array_equal(got.view(np.uint8), want.view(np.uint8), err_msg=str(i))
