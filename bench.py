@@ -194,7 +194,8 @@ def e2e_latency(cfg, n_calls):
         # done here so it can be timed apart; the suggest below then finds
         # nothing new
         t0 = time.perf_counter()
-        st.histories[t].sync(t).push(st.plan)
+        h = st.histories[t].sync(t)
+        h.push(st.plan_for(dom, h.n, st.plan.engine))   # (grows the plan as tpe.suggest does)
         t1 = time.perf_counter()
         docs = tpe.suggest(ids, dom, t, 100 + i, n_EI_candidates=n_c)
         t2 = time.perf_counter()
@@ -414,8 +415,11 @@ def report(args, C, eng, world, mode, elapsed, value, pairs_step, pairs_suggest,
     # roofline of the dominant kernel, k_score (every lpdf kind of a level
     # in one launch), priced at the measured register-only rate of exactly
     # its pair arithmetic (k_micro): log-sum-exp pairs and evaluated
-    # quantized pairs (the per-wave exact-zero skips cost no erf)
-    lse_peak = eng.microbench(3)
+    # quantized pairs (the per-wave exact-zero skips cost no erf).  LSE pairs
+    # are priced at the faster of the two pair sequences k_score has (per
+    # group max + lift, or one exponent per wave), whichever each wave ran
+    lse_peak_exact, lse_peak_shift = eng.microbench(3), eng.microbench(5)
+    lse_peak = max(lse_peak_exact, lse_peak_shift)
     erf_peak = eng.microbench(4)
     lse_pairs = kinds.get('lse_gmm', 0.0) + kinds.get('lse_lgmm', 0.0)
     per_launch = max(1, launches)
@@ -441,12 +445,14 @@ def report(args, C, eng, world, mode, elapsed, value, pairs_step, pairs_suggest,
                 note='unit = log-sum-exp-pair equivalents: achieved = (evaluated LSE pairs + '
                      'evaluated quantized pairs x lse_peak/erf_peak) / launch time; peaks are '
                      'register-only microkernels of exactly the pair arithmetic (LSE pair: 2 '
-                     'fp64 FMA + max + v_exp_f32 + fp64 sum, SURVEY 8d "1 exp + 6 flops"; '
-                     'quantized pair: 2 OCML fp64 erf + 8 flops)',
+                     'fp64 FMA + cvt + v_exp_f32 + fp32/fp64 sum with the wave exponent folded '
+                     'into alpha, SURVEY 8d "1 exp + 6 flops" -- the faster of it and the '
+                     'per-group-max form; quantized pair: 2 OCML fp64 erf + 8 flops)',
                 lse_pairs_per_launch=lse_pairs, lse_evaluated_pairs_per_launch=lse_exec,
                 erf_pairs_per_launch=kinds.get('erf_gmm', 0.0) + kinds.get('erf_lgmm', 0.0),
                 erf_evaluated_pairs_per_launch=erf_exec,
-                lse_pair_peak_per_s=lse_peak, erf_pair_peak_per_s=erf_peak,
+                lse_pair_peak_per_s=lse_peak, lse_pair_max_lift_peak_per_s=lse_peak_exact,
+                lse_pair_wave_exponent_peak_per_s=lse_peak_shift, erf_pair_peak_per_s=erf_peak,
                 fp64_fma_peak_flops=eng.microbench(1), exp_f32_peak_per_s=eng.microbench(0),
                 erf_f64_peak_per_s=eng.microbench(2))
     if lat_launches:

@@ -504,12 +504,14 @@ class Plan(object):
         with e.lock:
             e.check(e.lib.tpe_plan_set_lattice(self.p, int(bool(enable))))
 
-    def set_prune(self, enable):
-        """Skip provably-zero log-sum-exp component blocks on bucketed large
-        draws (default) or evaluate every pair (tpe_plan_set_prune)."""
+    def set_prune(self, mode):
+        """Log-sum-exp on bucketed large draws (tpe_plan_set_prune): 0 / False
+        every pair, 1 skip negligible component blocks, 2 / True (default)
+        skip + one exponent per wave."""
+        mode = 2 if mode is True else int(mode)
         e = self.engine
         with e.lock:
-            e.check(e.lib.tpe_plan_set_prune(self.p, int(bool(enable))))
+            e.check(e.lib.tpe_plan_set_prune(self.p, mode))
 
     def census(self, enable):
         """Pair census since the last call: (quantized total, live, evaluated,

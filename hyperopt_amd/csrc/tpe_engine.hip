@@ -22,6 +22,8 @@
 
 using namespace tpe;
 
+static int lse_shift_min();
+
 struct tpe_engine {
   int32_t device = 0;
   hipStream_t stream = nullptr;
@@ -72,7 +74,8 @@ struct tpe_plan {
   LatInfo *d_lat_info = nullptr;
   double2 *d_lat = nullptr;
   bool lattice_on = true;
-  bool prune_on = true;  // skip provably-zero log-sum-exp blocks (tpe_plan_set_prune)
+  int32_t prune_mode = 2;  // log-sum-exp on bucketed tiles (tpe_plan_set_prune): 0 full,
+                           // 1 block skip, 2 block skip + one exponent per wave
   hipEvent_t ev_fork = nullptr, ev_join[8] = {};
   double *d_ext = nullptr, *d_lb = nullptr, *d_la = nullptr;
   size_t ext_cap = 0;
@@ -656,7 +659,8 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
     const bool sorted_draw = !fuse_draw && table_draw &&
                              cn * n_sug * n_level >= ((int64_t)1 << 22);
     a.lse_pos = sorted_draw ? 1 : 0;
-    a.lse_prune = (sorted_draw && p->prune_on) ? 1 : 0;
+    a.lse_prune = sorted_draw ? p->prune_mode : 0;
+    a.lse_shift_min = lse_shift_min();
     if (fuse_draw) {
       tpe_plan::Prof *pr = nullptr;
       if (p->prof_cap > 0 && p->prof[1].n < p->prof_cap) pr = &p->prof[1];
@@ -1062,6 +1066,23 @@ int tpe_plan_update_history(tpe_plan_t p, int64_t n, int64_t row0, int64_t n_row
   if (loss0 < n && !losses) return fail(h, TPE_E_INVALID, "losses missing");
   CKH(hipSetDevice(h->device));
   hipStream_t st = pick_stream(h, stream);
+  const int64_t n_loss = n - loss0;
+  if (!on_device && n_rows * p->P <= kPatchVals && n_loss <= kPatchLoss) {
+    // the fmin steady state (a row or two, a few losses): the values ride in
+    // the kernel arguments -- no staging copy, no host synchronisation
+    HistPatch hp{};
+    hp.row0 = row0; hp.n_rows = n_rows; hp.loss0 = loss0; hp.n_loss = n_loss;
+    hp.ld = p->ncap; hp.P = p->P;
+    for (int i = 0; i < p->P; ++i)
+      for (int64_t r = 0; r < n_rows; ++r) {
+        hp.vals[i * n_rows + r] = vals[(int64_t)i * src_ld + r];
+        hp.active[i * n_rows + r] = active[(int64_t)i * src_ld + r];
+      }
+    for (int64_t i = 0; i < n_loss; ++i) hp.losses[i] = losses[i];
+    if (n_rows > 0 || n_loss > 0) CKH(launch_hist_patch(hp, p->d_vals, p->d_active, p->d_losses, st));
+    p->n = n;
+    return TPE_OK;
+  }
   const hipMemcpyKind kd = on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
   if (n_rows > 0 && p->P > 0) {
     CKH(hipMemcpy2DAsync(p->d_vals + row0, (size_t)p->ncap * 8, vals, (size_t)src_ld * 8,
@@ -1482,20 +1503,29 @@ int tpe_plan_sample_prior(tpe_plan_t p, const uint64_t *seeds, int64_t n_sug, tp
   return copy_results(h, p, n_sug, out, out_on_device, st);
 }
 
-int tpe_plan_set_prune(tpe_plan_t p, int32_t enable) {
-  if (!p) return TPE_E_INVALID;
-  if (p->prune_on != (enable != 0)) graph_reset(p);
-  p->prune_on = enable != 0;
+// lse_prune mode 2's smallest mixture (TPE_SHIFT_MIN_K overrides; tuning)
+static int lse_shift_min() {
+  static const int v = [] {
+    const char *e = std::getenv("TPE_SHIFT_MIN_K");
+    return e ? std::atoi(e) : 2048;
+  }();
+  return v;
+}
+
+int tpe_plan_set_prune(tpe_plan_t p, int32_t mode) {
+  if (!p || mode < 0 || mode > 2) return TPE_E_INVALID;
+  if (p->prune_mode != mode) graph_reset(p);
+  p->prune_mode = mode;
   return TPE_OK;
 }
 
 int tpe_microbench(tpe_handle_t h, int32_t which, double *per_second) {
-  if (!h || !per_second || which < 0 || which > 4) return TPE_E_INVALID;
+  if (!h || !per_second || which < 0 || which > 5) return TPE_E_INVALID;
   CKH(hipSetDevice(h->device));
   hipDeviceProp_t prop;
   CKH(hipGetDeviceProperties(&prop, h->device));
   const int blocks = prop.multiProcessorCount * 8;
-  const int iters = which == 2 ? 256 : (which == 3 ? 512 : (which == 4 ? 128 : 4096));
+  const int iters = which == 2 ? 256 : (which == 3 || which == 5 ? 512 : (which == 4 ? 128 : 4096));
   double *sink = nullptr;
   CKH(dalloc(&sink, (size_t)blocks * 256));
   hipEvent_t a, b;
@@ -1512,8 +1542,9 @@ int tpe_microbench(tpe_handle_t h, int32_t which, double *per_second) {
   (void)hipEventDestroy(b);
   dfree(sink);
   // results per thread-iteration: exp / FMA chains, erf chains, LSE pairs
-  // (4 candidates x 8 components), quantized pairs (2 chains)
-  static const double per_iter[5] = {8.0, 16.0, 4.0, 32.0, 2.0};
+  // (4 candidates x 8 components), quantized pairs (2 chains), shifted LSE
+  // pairs (4 x 8)
+  static const double per_iter[6] = {8.0, 16.0, 4.0, 32.0, 2.0, 32.0};
   *per_second = 4.0 * blocks * 256.0 * iters * per_iter[which] / (ms * 1e-3);
   return TPE_OK;
 }

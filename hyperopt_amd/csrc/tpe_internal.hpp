@@ -155,6 +155,7 @@ struct ScoreArgs {
   unsigned long long *census;  // optional [kCensus] pair counters (tpe_plan_census)
   int32_t lse_pos;           // LSE slots' candidates are value-bucketed (cand_pos valid)
   int32_t lse_prune;         // skip log-sum-exp blocks of exact-zero terms (needs lse_pos)
+  int32_t lse_shift_min;     // lse_prune 2: smallest mixture (components) for one wave exponent
   const LatInfo *lat_info;   // [P] value lattices (KIND_LAT slots)
   const double2 *lat;        // lattice (lpdf below, lpdf above) pairs
 };
@@ -245,6 +246,21 @@ hipError_t launch_sample(const tpe_hp *hp_dev, const double *mw,
                          hipStream_t st);
 
 hipError_t launch_micro(int which, int blocks, int iters, double *sink, hipStream_t st);
+
+// small history updates travel as kernel arguments (tpe_plan_update_history):
+// one launch, no staging copy and no host synchronisation
+constexpr int kPatchVals = 192;   // n_rows * P doubles / bytes
+constexpr int kPatchLoss = 16;    // losses
+struct HistPatch {
+  int64_t row0, n_rows, loss0, n_loss, ld;
+  int32_t P;
+  int32_t pad;
+  double vals[kPatchVals];        // [P][n_rows]
+  double losses[kPatchLoss];
+  uint8_t active[kPatchVals];     // [P][n_rows]
+};
+hipError_t launch_hist_patch(const HistPatch &h, double *vals, uint8_t *active, double *losses,
+                             hipStream_t st);
 
 // prior draws of whole suggestions (rand.suggest on the device): one block
 // per suggestion walks the levels of the compiled space

@@ -293,6 +293,28 @@ __global__ __launch_bounds__(256) void k_sample(const tpe_hp *__restrict__ hpd,
 }
 
 // ------------------------------------------------------------------------
+// history rows / losses carried in the kernel arguments (HistPatch)
+// ------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_hist_patch(HistPatch h, double *__restrict__ vals,
+                                                    uint8_t *__restrict__ active,
+                                                    double *__restrict__ losses) {
+  const int t = threadIdx.x;
+  const int cells = h.P * (int)h.n_rows;
+  for (int i = t; i < cells; i += blockDim.x) {
+    const int hp = i / (int)h.n_rows, r = i % (int)h.n_rows;
+    vals[(int64_t)hp * h.ld + h.row0 + r] = h.vals[i];
+    active[(int64_t)hp * h.ld + h.row0 + r] = h.active[i];
+  }
+  for (int i = t; i < (int)h.n_loss; i += blockDim.x) losses[h.loss0 + i] = h.losses[i];
+}
+
+hipError_t launch_hist_patch(const HistPatch &h, double *vals, uint8_t *active, double *losses,
+                             hipStream_t st) {
+  k_hist_patch<<<1, 256, 0, st>>>(h, vals, active, losses);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------
 // Prior draws (rand.suggest, hyperopt/rand.py:14-33, and the samplers of
 // pyll/stochastic.py:30-142): every active hp of a suggestion drawn from its
 // prior -- uniform / loguniform / quniform / qloguniform (the descriptor's
@@ -415,6 +437,40 @@ __global__ __launch_bounds__(256) void k_micro(int iters, double *sink) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) acc += sm[c] + m[c];
     if (acc == 12345.0) sink[t] = acc;
+  } else if constexpr (WHICH == 5) {
+    // one log-sum-exp pair as the one-exponent-per-wave loop computes it
+    // (lse_group_shifted): alpha - M once per component per lane, then two
+    // FMAs, cvt, exp2, fp32 tree, fp64 sum; 4 candidates x 8 components
+    double y[4], sm[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) { y[c] = 1e-3 * (t + c); sm[c] = 0.0; }
+    double cx[8], cy[8], cz[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { cx[k] = -0.1 * k; cy[k] = 0.01 * k; cz[k] = -0.5 - 0.01 * k; }
+    double M = 3.0;
+    for (int i = 0; i < iters; ++i) {
+      double am[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) am[k] = cx[k] - M;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float e[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          e[k] = __builtin_amdgcn_exp2f((float)fma(fma(cz[k], y[c], cy[k]), y[c], am[k]));
+#pragma unroll
+        for (int w = 4; w > 0; w >>= 1)
+#pragma unroll
+          for (int k = 0; k < w; ++k) e[k] += e[k + w];
+        sm[c] += (double)e[0];
+        y[c] += 1e-9;
+      }
+      M += 1e-12;
+    }
+    double acc = 0.0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc += sm[c];
+    if (acc == 12345.0) sink[t] = acc;
   } else if constexpr (WHICH == 4) {
     // one quantized pair exactly as k_score computes a live one: two OCML
     // fp64 erf, the reference's Phi and two-stage increment; 2 chains
@@ -458,6 +514,7 @@ hipError_t launch_micro(int which, int blocks, int iters, double *sink, hipStrea
     case 1: k_micro<1><<<blocks, 256, 0, st>>>(iters, sink); break;
     case 3: k_micro<3><<<blocks, 256, 0, st>>>(iters, sink); break;
     case 4: k_micro<4><<<blocks, 256, 0, st>>>(iters, sink); break;
+    case 5: k_micro<5><<<blocks, 256, 0, st>>>(iters, sink); break;
     default: k_micro<2><<<blocks, 256, 0, st>>>(iters, sink); break;
   }
   return hipGetLastError();

@@ -230,6 +230,132 @@ __device__ __forceinline__ void lse_chunks(KDbl *__restrict__ cs, const Coef *__
   }
 }
 
+// Shifted log-sum-exp over the live blocks (value-bucketed tiles): one
+// exponent M for the whole wave instead of a per-group max and lift.  M =
+// ceil(largest live block bound over the wave's range) + 1 is an upper bound
+// of every term of every lane, so t - M <= 0 and alpha - M is folded into
+// the coefficients once per component (shared by the lane's candidates): a
+// pair costs 2 fp64 FMA + cvt + v_exp_f32 + an fp32 add.  Accuracy guard: the
+// fp32 rounding of t - M costs |t - M| * 2^-24 relative per term, so every
+// valid lane's sum must be >= 2^-4 (its dominant terms within ~4 of M, error
+// <= 3e-7); otherwise (a spread-out tile) the wave returns false and the
+// exact per-group-lift loop runs instead.
+template <int KR>
+__device__ __forceinline__ void lse_group_shifted(const CoefGroup &g, double M,
+                                                  const double (&y)[KR], double (&s)[KR]) {
+  // two halves of 4 components: the shifted alphas and the fp32 terms of a
+  // half stay in few VGPRs; a lane's group sum is (h0 tree) + (h1 tree)
+  float f[KR];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    double am[kGroup / 2];
+#pragma unroll
+    for (int j = 0; j < kGroup / 2; ++j) am[j] = g.x[4 * h + j] - M;
+#pragma unroll
+    for (int r = 0; r < KR; ++r) {
+      float e[kGroup / 2];
+#pragma unroll
+      for (int j = 0; j < kGroup / 2; ++j)
+        e[j] = __builtin_amdgcn_exp2f(
+            (float)fma(fma(g.z[4 * h + j], y[r], g.y[4 * h + j]), y[r], am[j]));
+      const float t = (e[0] + e[2]) + (e[1] + e[3]);
+      f[r] = h ? f[r] + t : t;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < KR; ++r) s[r] += (double)f[r];
+}
+
+template <int KR, bool CENSUS>
+__device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
+                                                   const Coef *__restrict__ cv, int c0, int nb,
+                                                   const double (&y)[KR], const bool (&valid)[KR],
+                                                   LseAcc (&out)[KR], LseWindow win, int nvalid,
+                                                   LseCensus &cen) {
+  const int lane = threadIdx.x & 63;
+  const int nch = (nb + kChunk - 1) / kChunk;
+  const double *tb = reinterpret_cast<const double *>(cv);
+  // pass 1: the largest live block bound of the wave's chunks
+  float bmax = -INFINITY;
+  for (int r0 = c0; r0 < nch; r0 += kWaves * 64) {
+    const int c = r0 + kWaves * lane;
+    const int k0 = c * kChunk;
+    if (c < nch) {
+      const float b0 = envelope_bound(*reinterpret_cast<const float4 *>(tb + coef_off(k0, 3)), win);
+      if (b0 >= win.thr) bmax = fmaxf(bmax, b0);
+      if (k0 + kGroup < nb) {
+        const float b1 =
+            envelope_bound(*reinterpret_cast<const float4 *>(tb + coef_off(k0 + kGroup, 3)), win);
+        if (b1 >= win.thr) bmax = fmaxf(bmax, b1);
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) bmax = fmaxf(bmax, __shfl_xor(bmax, o, 64));
+  if (!(bmax > -INFINITY && bmax < INFINITY)) return false;  // non-finite envelope
+  // pass 2 with M = ceil(bmax) + 1 for every lane; a lane whose sum comes
+  // out below 2^-4 re-centres on its own sum (M + ceil(log2 s) + 1, the sum
+  // then in (1/4, 1/2]) and the wave runs once more; failing that (or a sum
+  // that underflowed), the exact loop
+  double M = __builtin_amdgcn_readfirstlane((int)ceil((double)bmax)) + 1.0;
+  double s[KR];
+  for (int attempt = 0;; ++attempt) {
+#pragma unroll
+    for (int r = 0; r < KR; ++r) s[r] = 0.0;
+    for (int r0 = c0; r0 < nch; r0 += kWaves * 64) {
+      const int c = r0 + kWaves * lane;
+      const int k0 = c * kChunk;
+      const bool has0 = c < nch, has1 = has0 && k0 + kGroup < nb;
+      bool live0 = false, live1 = false;
+      if (has0) {
+        live0 =
+            envelope_bound(*reinterpret_cast<const float4 *>(tb + coef_off(k0, 3)), win) >= win.thr;
+        if (has1)
+          live1 = envelope_bound(*reinterpret_cast<const float4 *>(tb + coef_off(k0 + kGroup, 3)),
+                                 win) >= win.thr;
+      }
+      if constexpr (CENSUS) {
+        const int n0 = has0 ? min(kGroup, nb - k0) : 0,
+                  n1 = has1 ? min(kGroup, nb - k0 - kGroup) : 0;
+        uint32_t tot = (uint32_t)(n0 + n1), ex = (uint32_t)((live0 ? n0 : 0) + (live1 ? n1 : 0));
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          tot += __shfl_xor(tot, o, 64);
+          ex += __shfl_xor(ex, o, 64);
+        }
+        if (attempt == 0) cen.total += tot * (uint32_t)nvalid;
+        cen.exec += ex * (uint32_t)nvalid;
+      }
+      uint64_t m0 = __ballot(live0), m1 = __ballot(live1);
+      while (m0 | m1) {
+        const int j0 = m0 ? __builtin_ctzll(m0) : 64, j1 = m1 ? __builtin_ctzll(m1) : 64;
+        const int g = j1 < j0 ? 1 : 0;
+        const int j = g ? j1 : j0;
+        if (g) m1 &= m1 - 1;
+        else m0 &= m0 - 1;
+        CoefGroup cgp;
+        load_group(cs, (r0 + kWaves * j) * kChunk + g * kGroup, cgp);
+        lse_group_shifted<KR>(cgp, M, y, s);
+      }
+    }
+    bool ok = true;
+    double smax = 0.0;
+#pragma unroll
+    for (int r = 0; r < KR; ++r)
+      if (valid[r] && y[r] == y[r]) {
+        ok &= s[r] >= 0.0625;
+        smax = fmax(smax, s[r]);
+      }
+    if (__all(ok)) break;
+    if (attempt > 0 || !__all(ok || smax >= 0x1p-100)) return false;
+    // lanes that fit keep M (identical second pass); the others re-centre
+    if (!ok) M += ceil(log2(smax)) + 1.0;
+  }
+#pragma unroll
+  for (int r = 0; r < KR; ++r) out[r] = (y[r] != y[r]) ? LseAcc{NAN, NAN} : LseAcc{M, s[r]};
+  return true;
+}
+
 // PRUNE setup: the wave's candidate range and, from the mixture's probe
 // component (its widest, the Parzen prior), a lower bound on every lane's
 // final exponent m (m >= max_k t_k >= t_probe).  Non-finite candidates or a
@@ -524,8 +650,17 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
         const bool prune = A.lse_prune != 0;
         LseWindow win{0.0f, 0.0f, -INFINITY};
         if (prune) win = lse_window<KR>(uniform_ptr(cm), mix ? ia.probe : ib.probe, K, y, valid);
-        lse_chunks<KR, CENSUS>(uniform_ptr(cm), cm, wv, K, y, lacc[mix], prune, win, nvalid,
-                               lcen);
+        // shifted single-exponent loop when the wave's window allows it
+        // (lse_chunks_shifted's guard), else the exact per-group-lift loop
+        // (mixtures of >= lse_shift_min components: fewer leave too few
+        // terms near a wave-wide exponent for most waves to pass its guard)
+        const bool shifted = prune && A.lse_prune > 1 && K >= A.lse_shift_min &&
+                             win.thr > -INFINITY &&
+                             lse_chunks_shifted<KR, CENSUS>(uniform_ptr(cm), cm, wv, K, y, valid,
+                                                            lacc[mix], win, nvalid, lcen);
+        if (!shifted)
+          lse_chunks<KR, CENSUS>(uniform_ptr(cm), cm, wv, K, y, lacc[mix], prune, win, nvalid,
+                                 lcen);
       } else {
         erf_chunks<KR, LOGN, CENSUS>(uniform_ptr(cm), wv, K, ub, lb, valid, wlo, whi, exact, pacc[mix], cen);
       }

@@ -258,18 +258,21 @@ int tpe_plan_census(tpe_plan_t p, int32_t enable, int64_t *counts);
 int tpe_plan_sample_prior(tpe_plan_t p, const uint64_t *seeds, int64_t n_suggest,
                           tpe_result *out, int32_t out_on_device, void *stream);
 
-/* Large draws score log-sum-exp candidates on value-bucketed tiles and skip
- * the blocks of 8 mixture components whose every term is below
+/* Large draws score log-sum-exp candidates on value-bucketed tiles.  mode 1
+ * skips the blocks of 8 mixture components whose every term is below
  * 2^-(31 + log2 K) of each candidate's largest one (lpdf moved by <= 2^-30
- * ~ 1e-9 relative).
- * enable = 0 evaluates every (candidate, component) pair, for A/B
- * measurement and tests.                                                   */
-int tpe_plan_set_prune(tpe_plan_t p, int32_t enable);
+ * ~ 1e-9 relative); mode 2 (default) also gives each wave one exponent
+ * instead of a per-group max (terms 2^(t - M), M an upper bound of the
+ * wave's terms), guarded so no term's fp32 argument exceeds ~|4| where it
+ * matters (<= 3e-7 relative; else the wave falls back to mode 1).  mode 0
+ * evaluates every (candidate, component) pair -- A/B measurement, tests.   */
+int tpe_plan_set_prune(tpe_plan_t p, int32_t mode);
 
 /* Register-only microbenchmarks for the roofline: which = 0 v_exp_f32
  * (results/s), 1 fp64 FMA (flop/s), 2 OCML fp64 erf (results/s), 3 the
  * log-sum-exp (candidate, component) pair of the scoring kernel (pairs/s),
- * 4 a live quantized pair (2 fp64 erf; pairs/s).                           */
+ * 4 a live quantized pair (2 fp64 erf; pairs/s), 5 the log-sum-exp pair of
+ * the one-exponent-per-wave loop (tpe_plan_set_prune mode 2; pairs/s).      */
 int tpe_microbench(tpe_handle_t h, int32_t which, double *per_second);
 
 #ifdef __cplusplus

@@ -35,3 +35,17 @@ def argmax_equiv(score_ref, idx_got, rtol=RTOL):
     if np.isnan(b):
         return False
     return np.isfinite(a) and abs(a - b) <= rtol * max(1.0, abs(b))
+
+
+def assert_winners_match(got, want, rtol=RTOL, msg=''):
+    """Two runs' per-hp winners (RESULT_DTYPE rows) agree under the north
+    star tie rule: same index and value, or -- where the runs' scoring
+    rounded differently (other tiling, one exponent per wave) -- different
+    winners whose scores tie within tolerance (each run's winner scores at
+    least the other's, so |delta| <= the scoring error bound)."""
+    got, want = np.asarray(got).reshape(-1), np.asarray(want).reshape(-1)
+    np.testing.assert_array_equal(got['active'], want['active'], err_msg=msg)
+    same = got['index'] == want['index']
+    np.testing.assert_array_equal(got['value'][same], want['value'][same], err_msg=msg)
+    assert_close(got['score'], want['score'], rtol, msg=msg)
+    return int((~same).sum())

@@ -412,25 +412,31 @@ def test_thread_trials_async_batched_tpe():
 def test_pruned_lse_equals_full_evaluation(name):
     """Large draws (>= 4M candidate draws) are value-bucketed by the draw and
     log-sum-exp tiles skip the component blocks whose terms are all below
-    2^-(31 + log2 K) of every candidate's largest: winners (index, value)
-    equal the unpruned run and scores agree within 2^-30 relative per lpdf;
-    the winner also equals the merge of two differently tiled shards."""
+    2^-(31 + log2 K) of every candidate's largest (mode 1): winners (index,
+    value) equal the unpruned run and scores agree within 2^-30 relative per
+    lpdf.  Mode 2 (default) also gives each wave one exponent: scores within
+    the north-star 1e-6, winners equal up to ties within it.  The winner also
+    equals the merge of two differently tiled shards."""
     torch = pytest.importorskip('torch')
+    from gpu_util import assert_winners_match
     meta, d, dom, trials = _fixture_trials(name)
     tpe.suggest([meta['new_id']], dom, trials, 7, n_EI_candidates=64)
     plan = dom._tpe_state.plan
     n = 1 << 18 if name == 'cfg2' else 1 << 20
-    plan.set_prune(True)
+    plan.set_prune(1)
     plan.census(True)
     got = plan.suggest([21, 22], n)
     c = plan.census(False)
-    plan.set_prune(False)
+    plan.set_prune(2)
+    shifted = plan.suggest([21, 22], n)
+    plan.set_prune(0)
     want = plan.suggest([21, 22], n)
-    plan.set_prune(True)
+    plan.set_prune(2)
     np.testing.assert_array_equal(got['index'], want['index'])
     np.testing.assert_array_equal(got['value'], want['value'])
     np.testing.assert_array_equal(got['active'], want['active'])
     np.testing.assert_allclose(got['score'], want['score'], rtol=4e-9, atol=4e-9)
+    assert_winners_match(shifted, want, msg='one exponent per wave')
     assert c[3] > 0 and c[5] < c[3], c          # blocks were skipped
     if name != 'cfg2':
         return                                   # one level: shards merge directly
@@ -439,8 +445,7 @@ def test_pruned_lse_equals_full_evaluation(name):
     raw = torch.from_numpy(np.stack(parts).view(np.uint8).reshape(-1).copy()).cuda()
     merged = plan.merge(raw.data_ptr(), world=2, level=0)
     torch.cuda.synchronize()
-    np.testing.assert_array_equal(merged[0]['index'], got[0]['index'])
-    np.testing.assert_array_equal(merged[0]['value'], got[0]['value'])
+    assert_winners_match(merged[0], shifted[0], msg='shard merge')
 
 
 def test_graph_replay_across_fused_draw_threshold():

@@ -1,5 +1,6 @@
-"""A/B of the log-sum-exp block skip on a BASELINE config (device time per
-suggest, census of evaluated pairs).  Diagnostic: python tools/ab_prune.py cfg4"""
+"""A/B of the log-sum-exp modes (tpe_plan_set_prune: 2 skip + one exponent
+per wave, 1 skip, 0 every pair) on a BASELINE config (time per suggest,
+census of evaluated pairs, max |delta score| vs mode 0).  Diagnostic: python tools/ab_prune.py cfg4"""
 import json
 import os
 import sys
@@ -25,21 +26,25 @@ def main():
     plan.set_history(losses, vals, active)
     seeds = [7] if cfg != 'cfg5' else list(range(16))
     out = {}
-    for prune in (True, False):
-        plan.set_prune(prune)
+    res = {}
+    for mode in (2, 1, 0):
+        plan.set_prune(mode)
         plan.fit_suggest(seeds, n_cand)            # warm
         t0 = time.perf_counter()
         for i in range(reps):
             r = plan.fit_suggest([s + 100 * i for s in seeds], n_cand)
         dt = (time.perf_counter() - t0) / reps
         plan.census(True)
-        plan.fit_suggest(seeds, n_cand)
+        res[mode] = plan.fit_suggest(seeds, n_cand)
         c = plan.census(False)
-        out['prune' if prune else 'full'] = dict(ms=1e3 * dt, census=c,
-                                                 lse_eval_frac=c[5] / max(1, c[3]))
-        print(json.dumps({('prune' if prune else 'full'): out['prune' if prune else 'full']}),
-              flush=True)
-    out['speedup'] = out['full']['ms'] / out['prune']['ms']
+        out['mode%d' % mode] = dict(ms=1e3 * dt, census=c, lse_eval_frac=c[5] / max(1, c[3]))
+        print(json.dumps({'mode%d' % mode: out['mode%d' % mode]}), flush=True)
+    for mode in (2, 1):
+        a, b = res[mode], res[0]
+        out['mode%d' % mode].update(
+            speedup=out['mode0']['ms'] / out['mode%d' % mode]['ms'],
+            index_diff=int((a['index'] != b['index']).sum()),
+            max_abs_dscore=float(np.nanmax(np.abs(a['score'] - b['score']))))
     print(json.dumps(out))
 
 
