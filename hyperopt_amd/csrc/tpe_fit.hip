@@ -35,7 +35,7 @@ namespace tpe {
 #ifdef TPE_STAMPS
 // diagnostic build only (make dbg; tools/fit_stamps.py): per-slot phase
 // timestamps of k_fit, wall clock (100 MHz)
-__device__ unsigned long long g_stamps[512][16];
+__device__ unsigned long long g_stamps[512][48];  // [0, 16) phases, [16, 48) sub-phases
 #define STAMP(ph)                                                             \
   do {                                                                        \
     if (threadIdx.x == 0 && blockIdx.z == 0)                                  \
@@ -108,22 +108,9 @@ __device__ __forceinline__ uint32_t wave_excl_scan_u32(uint32_t v) {
   return x - v;
 }
 
-// block-wide sum of small ints (one barrier pair)
-__device__ int block_sum_int(int v, int *buf) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  if (lane == 0) buf[w] = v;
-  __syncthreads();
-  int t = 0;
-#pragma unroll
-  for (int i = 0; i < kFitWaves; ++i) t += buf[i];
-  __syncthreads();
-  return t;
-}
-
-// block-wide exclusive scan of small ints; total returned by reference
-__device__ NOINLINE int block_excl_scan(int v, int *wsum, int &total) {
+// block-wide exclusive scan of small ints: (exclusive prefix, total) -- by
+// value, in registers (an out-reference of a call lives on the scratch stack)
+__device__ NOINLINE int2 block_excl_scan(int v, int *wsum) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   int x = v;
 #pragma unroll
@@ -140,9 +127,8 @@ __device__ NOINLINE int block_excl_scan(int v, int *wsum, int &total) {
     before += (i < w) ? s : 0;
     tot += s;
   }
-  total = tot;
   __syncthreads();
-  return before + x - v;
+  return make_int2(before + x - v, tot);
 }
 
 // lanes of this wave whose 8-bit digit equals mine (among lanes with v set)
@@ -246,10 +232,13 @@ __device__ void merge_sort_1024(const uint64_t *keys, int n, uint16_t *out, uint
   const int t = threadIdx.x;
   uint64_t k = t < n ? keys[t] : ~0ull;
   uint32_t p = (uint32_t)t;  // padding (~0, t >= n): distinct, after every real key
+  STAMP(21);
   wave_bitonic64(k, p);
+  STAMP(22);
   bk0[t] = k;
   bp0[t] = (uint16_t)p;
   __syncthreads();
+  STAMP(23);
   uint64_t *sk = bk0, *dk = bk1;
   uint16_t *sp = bp0, *dp = bp1;
   for (int len = 64; len < kFitThreads; len <<= 1) {
@@ -269,18 +258,97 @@ __device__ void merge_sort_1024(const uint64_t *keys, int n, uint16_t *out, uint
     uint16_t *tp = sp; sp = dp; dp = tp;
     k = sk[t];  // this thread now owns merged position t
     p = sp[t];
+    STAMP(24 + (__builtin_ctz((unsigned)len) - 6));
   }
   if (t < n) out[t] = sp[t];
   __syncthreads();
 }
 
+// The same sort on one packed word per element: 32 key bits (from the lowest
+// bit that varies over the keys, or up to the highest one: the bits outside
+// are equal for all) above the position, so a step is one 64-bit compare and
+// one exchange instead of a (key, position) pair.  Exact when no varying bit
+// is dropped (!lossy); otherwise a run of equal truncated keys is ordered by
+// position, so each such run (rare, short) is re-ranked by its full keys;
+// false (the caller then sorts the full keys) for a run of more than kRunMax.
+__device__ void wave_bitonic64_packed(uint64_t &k) {
+  const int lane = threadIdx.x & 63;
+  for (int kk = 2; kk <= 64; kk <<= 1) {
+    for (int j = kk >> 1; j > 0; j >>= 1) {
+      const bool asc = (lane & kk) == 0 || kk == 64;
+      const uint64_t ok = __shfl_xor(k, j, 64);
+      const bool lower = (lane & j) == 0;
+      const bool other_less = ok < k;
+      if ((lower == asc) ? other_less : !other_less) k = ok;
+    }
+  }
+}
+
+__device__ bool merge_sort_1024_packed(const uint64_t *keys, int n, int shift, bool lossy,
+                                       uint16_t *out, uint64_t *b0, uint64_t *b1) {
+  const int t = threadIdx.x;
+  // padding (t >= n): all-ones key bits, position t > every real position
+  uint64_t k = (t < n ? ((keys[t] >> shift) << 32) : 0xFFFFFFFF00000000ull) | (uint64_t)t;
+  wave_bitonic64_packed(k);
+  b0[t] = k;
+  __syncthreads();
+  uint64_t *sk = b0, *dk = b1;
+  for (int len = 64; len < kFitThreads; len <<= 1) {
+    const int run = t / len, idx = t % len;
+    const int other = (run ^ 1) * len;
+    int lo = 0, hi = len;  // lower bound of k in the partner run (all words distinct)
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (sk[other + mid] < k) lo = mid + 1;
+      else hi = mid;
+    }
+    dk[(run & ~1) * len + idx + lo] = k;
+    __syncthreads();
+    uint64_t *tk = sk; sk = dk; dk = tk;
+    k = sk[t];  // this thread now owns merged position t
+  }
+  // runs of equal truncated keys (sorted by position so far) are ranked by
+  // their full keys; a run longer than kRunMax sends the block to the full sort
+  constexpr int kRunMax = 16;
+  const uint32_t p = (uint32_t)k;
+  bool bad = false;
+  if (t < n) {
+    int s0 = t, s1 = t + 1;
+    if (lossy) {
+      const uint32_t hk = (uint32_t)(k >> 32);
+      while (s0 > 0 && t - s0 < kRunMax && (uint32_t)(sk[s0 - 1] >> 32) == hk) --s0;
+      while (s1 < n && s1 - t <= kRunMax && (uint32_t)(sk[s1] >> 32) == hk) ++s1;
+    }
+    if (s1 - s0 > kRunMax) {
+      bad = true;
+    } else if (s1 - s0 == 1) {
+      out[t] = (uint16_t)p;
+    } else {
+      const uint64_t kf = keys[p];
+      int r = 0;
+      for (int u = s0; u < s1; ++u) {
+        const uint32_t pu = (uint32_t)sk[u];
+        r += kp_less(keys[pu], pu, kf, p) ? 1 : 0;
+      }
+      out[s0 + r] = (uint16_t)p;
+    }
+  }
+  return !__syncthreads_or(bad);
+}
+
 template <typename PosT>
-__device__ PosT *block_sort_perm(const uint64_t *keys, PosT *a, PosT *b, int n, uint32_t *cnt,
-                                 uint32_t *run, FitShared &sm) {
+__device__ PosT *block_sort_perm(const uint64_t *keys, PosT *a, PosT *b, int n, uint64_t vary,
+                                 uint32_t *cnt, uint32_t *run, FitShared &sm) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (n > 64 && n <= kMergeMax && sizeof(PosT) == 2) {
     // cnt + run regions (32 KB) hold the two key buffers, b the positions
     uint64_t *bk = reinterpret_cast<uint64_t *>(cnt);
+    // the 32-bit window: from the lowest varying bit, or up to the highest
+    const int hb = 63 - __builtin_clzll(vary | 1ull), lb = vary ? __builtin_ctzll(vary) : 0;
+    const int shift = max(lb, hb - 31);
+    if (merge_sort_1024_packed(keys, n, shift, shift > lb, reinterpret_cast<uint16_t *>(a), bk,
+                               bk + kFitThreads))
+      return a;
     uint16_t *bp = reinterpret_cast<uint16_t *>(b);
     merge_sort_1024(keys, n, reinterpret_cast<uint16_t *>(a), bk, bp, bk + kFitThreads,
                     bp + kFitThreads);
@@ -296,25 +364,8 @@ __device__ PosT *block_sort_perm(const uint64_t *keys, PosT *a, PosT *b, int n, 
     __syncthreads();
     return a;
   }
-  uint64_t an = ~0ull, on = 0ull;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    a[i] = (PosT)i;
-    const uint64_t k = keys[i];
-    an &= k;
-    on |= k;
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    an &= __shfl_xor(an, o, 64);
-    on |= __shfl_xor(on, o, 64);
-  }
-  if (lane == 0) { sm.vand[w] = an; sm.vor[w] = on; }
+  for (int i = threadIdx.x; i < n; i += blockDim.x) a[i] = (PosT)i;
   __syncthreads();
-  an = ~0ull;
-  on = 0ull;
-#pragma unroll
-  for (int i = 0; i < kFitWaves; ++i) { an &= sm.vand[i]; on |= sm.vor[i]; }
-  const uint64_t vary = an ^ on;
   for (int shift = 0; shift < 64; shift += 8) {
     if (((vary >> shift) & 255u) == 0) continue;
     radix_pass<PosT>(keys, a, b, n, shift, cnt, run);
@@ -418,6 +469,7 @@ __device__ __forceinline__ void block_np_sums(const double *const (&arr)[NA], in
     __syncthreads();
     if (threadIdx.x < 64 && P.n != cn) np_plan(cn, P);
     __syncthreads();
+    STAMP(28);
     const int nl = P.n_leaves;
     for (int g0 = 0; g0 < nl; g0 += groups) {  // uniform trip count
       const int g = g0 + (threadIdx.x >> 3);
@@ -452,6 +504,7 @@ __device__ __forceinline__ void block_np_sums(const double *const (&arr)[NA], in
       }
     }
     __syncthreads();
+    STAMP(29);
     if (threadIdx.x < 64) {
       np_combine_wave<NA>(P, sm.val);
       if (threadIdx.x == 0) {
@@ -462,6 +515,7 @@ __device__ __forceinline__ void block_np_sums(const double *const (&arr)[NA], in
     }
   }
   __syncthreads();
+  STAMP(30);
 #pragma unroll
   for (int q = 0; q < NA; ++q) out[q] = n > 0 ? sm.total2[q] : 0.0;
   __syncthreads();
@@ -528,8 +582,22 @@ struct FitCtx {
 };
 
 struct Digit {
-  uint32_t d;    // selected digit
-  uint32_t cnt;  // values with that digit (under the prefix)
+  uint32_t d;     // selected digit
+  uint32_t cnt;   // values with that digit (under the prefix)
+  uint32_t need;  // the rank sought, inside that digit
+};
+
+// select_digit's value functions, passed by value (in registers: a lambda
+// capturing by reference would put its captures on the scratch stack and
+// make every value a scratch load)
+struct KeyAt {
+  const uint64_t *keys;
+  __device__ uint64_t operator()(int j) const { return keys[j]; }
+};
+struct TiedPosAt {  // positions of the trials whose key equals T
+  const uint64_t *keys;
+  uint64_t T;
+  __device__ uint64_t operator()(int j) const { return keys[j] == T ? (uint64_t)j : ~0ull; }
 };
 
 // One radix-select step: histogram (wave-aggregated LDS atomics) of the
@@ -538,12 +606,13 @@ struct Digit {
 // becomes the rank inside that digit.
 template <typename ValFn>
 __device__ NOINLINE Digit select_digit(ValFn val, int n, uint64_t mask, uint64_t prefix, int shift,
-                              uint32_t &need, uint32_t *hist, FitShared &sm, int par) {
+                                       uint32_t need, uint32_t *hist, FitShared &sm, int par) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   // hist[0..256) is zero on entry; zero the other half for the next step
   // (nobody reads it before this step's first barrier)
   uint32_t *other = par ? hist - kDigits : hist + kDigits;
   for (int d = threadIdx.x; d < kDigits; d += blockDim.x) other[d] = 0;
+  STAMP(16);
   for (int j0 = 0; j0 < n; j0 += blockDim.x) {
     const int j = j0 + threadIdx.x;
     const uint64_t x = j < n ? val(j) : 0ull;
@@ -552,7 +621,9 @@ __device__ NOINLINE Digit select_digit(ValFn val, int n, uint64_t mask, uint64_t
     const uint64_t mt = match8(d, v);
     if (v && lane == __ffsll((long long)mt) - 1) atomicAdd(&hist[d], (uint32_t)__popcll(mt));
   }
+  STAMP(17);
   __syncthreads();
+  STAMP(18);
   if (w == 0) {
     const uint4 c = *reinterpret_cast<const uint4 *>(hist + 4 * lane);
     const uint32_t ls = c.x + c.y + c.z + c.w;
@@ -571,10 +642,10 @@ __device__ NOINLINE Digit select_digit(ValFn val, int n, uint64_t mask, uint64_t
       sm.rp[par][2] = cnt;
     }
   }
+  STAMP(19);
   __syncthreads();
-  const Digit r{sm.rp[par][0], sm.rp[par][2]};
-  need = sm.rp[par][1];
-  return r;
+  STAMP(20);
+  return Digit{sm.rp[par][0], sm.rp[par][2], sm.rp[par][1]};
 }
 
 // (a2) the n_below-th smallest (loss key, position) by radix select over the
@@ -613,13 +684,14 @@ __device__ Split compute_split(const FitArgs &A, const FitCtx &C, FitShared &sm)
   uint64_t mask = ~vary, prefix = an & ~vary;  // constant digits are known
   uint32_t need = (uint32_t)nb, eq = (uint32_t)n;
   int step = 0;
-  auto kv = [&](int j) { return keys[j]; };
+  const KeyAt kv{keys};
   for (int shift = 56; shift >= 0; shift -= 8) {
     const uint64_t dm = 255ull << shift;
     if ((vary & dm) == 0) continue;
     const Digit g = select_digit(kv, n, mask, prefix, shift, need, hist + kDigits * (step & 1),
                                  sm, step & 1);
     ++step;
+    need = g.need;
     prefix |= (uint64_t)g.d << shift;
     mask |= dm;
     eq = g.cnt;
@@ -632,11 +704,12 @@ __device__ Split compute_split(const FitArgs &A, const FitCtx &C, FitShared &sm)
   if (need == eq) return Split{prefix, ~0u, 2};
   const uint64_t T = prefix;
   uint64_t pmask = 0, pprefix = 0;
-  auto pv = [&](int j) { return keys[j] == T ? (uint64_t)j : ~0ull; };
+  const TiedPosAt pv{keys, T};
   for (int shift = 24; shift >= 0; shift -= 8) {
     const Digit g = select_digit(pv, n, pmask | 0xFFFFFFFF00000000ull, pprefix, shift, need,
                                  hist + kDigits * (step & 1), sm, step & 1);
     ++step;
+    need = g.need;
     pprefix |= (uint64_t)g.d << shift;
     pmask |= 255ull << shift;
   }
@@ -875,9 +948,23 @@ __device__ void fit_categorical(const FitArgs &A, const FitCtx &C, FitShared &sm
 // ------------------------------------------------------------------------
 // k_fit: split + fit + lpdf constants, one block per (hp, side)
 // ------------------------------------------------------------------------
+#ifndef TPE_FIT_REPS
+#define TPE_FIT_REPS 1  // diagnostic builds: > 1 repeats the fit (warm caches)
+#endif
+__device__ __forceinline__ void fit_slot(const FitArgs &A, unsigned char *dyn_lds,
+                                         FitShared &sm);
+
 __global__ __launch_bounds__(kFitThreads) void k_fit(FitArgs A) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn_lds[];
   __shared__ FitShared sm;
+  for (int rep = 0; rep < TPE_FIT_REPS; ++rep) {
+    fit_slot(A, dyn_lds, sm);
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ void fit_slot(const FitArgs &A, unsigned char *dyn_lds,
+                                         FitShared &sm) {
   const int hp = blockIdx.x, side = blockIdx.y;  // side 0 = below ("good")
   const int64_t slot = 2 * (int64_t)hp + side;
   const tpe_hp H = A.hps[hp];
@@ -889,6 +976,9 @@ __global__ __launch_bounds__(kFitThreads) void k_fit(FitArgs A) {
   C.gpa = reinterpret_cast<uint32_t *>(gsb + 8 * A.scap);
   C.gpb = C.gpa + A.scap;
   STAMP(0);
+#ifdef TPE_STAMPS
+  const unsigned long long clk0 = clock64();  // shader clock: SCLK = cycles / wall time
+#endif
   const Split t = compute_split(A, C, sm);
   __syncthreads();
   STAMP(1);
@@ -898,9 +988,14 @@ __global__ __launch_bounds__(kFitThreads) void k_fit(FitArgs A) {
   const bool cat = H.family == TPE_CAT;
   const double *row = A.vals + (int64_t)hp * A.ld;
   const uint8_t *arow = A.active + (int64_t)hp * A.ld;
-  double *ob = A.ob + slot * A.kcap;
+  // observations: LDS above the keys when the history is small (no global
+  // stores in flight at the barriers that follow), else slot scratch
+  double *ob = A.n <= kMergeMax
+                   ? reinterpret_cast<double *>(dyn_lds + kOffKeys + 8 * kMergeMax)
+                   : A.ob + slot * A.kcap;
   uint64_t *lk = reinterpret_cast<uint64_t *>(dyn_lds + kOffKeys);
   int m = 0, nlt = 0;
+  uint64_t kand = ~0ull, kor = 0ull;  // bits equal over all keys: kand == kor there
   for (int64_t c0 = 0; c0 < A.n; c0 += 4 * kFitThreads) {
     const int64_t j0 = c0 + 4 * (int64_t)threadIdx.x;
     bool f[4];
@@ -927,20 +1022,37 @@ __global__ __launch_bounds__(kFitThreads) void k_fit(FitArgs A) {
       }
       cntl += f[u] ? 1 : 0;
     }
-    int tot;
-    int i = m + block_excl_scan(cntl, sm.wsum, tot);
+    const int2 sc = block_excl_scan(cntl, sm.wsum);
+    const int tot = sc.y;
+    int i = m + sc.x;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (!f[u]) continue;
       ob[i] = v[u];
       const uint64_t k = cat ? (uint64_t)(int64_t)v[u] : sort_key(v[u]);
+      kand &= k;
+      kor |= k;
       if (i < kSortCap) lk[i] = k;
       else C.gkeys[i] = k;
       ++i;
     }
     m += tot;
   }
-  nlt = block_sum_int(nlt, sm.isum);
+  {  // block reductions: nlt, and the varying key bits for the sort
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      nlt += __shfl_xor(nlt, o, 64);
+      kand &= __shfl_xor(kand, o, 64);
+      kor |= __shfl_xor(kor, o, 64);
+    }
+    if (lane == 0) { sm.isum[w] = nlt; sm.vand[w] = kand; sm.vor[w] = kor; }
+    __syncthreads();
+    nlt = 0;
+#pragma unroll
+    for (int i = 0; i < kFitWaves; ++i) { nlt += sm.isum[i]; kand &= sm.vand[i]; kor |= sm.vor[i]; }
+  }
+  const uint64_t vary = kand ^ kor;
   const bool lds_sort = m <= kSortCap;
   if (!lds_sort)
     for (int i = threadIdx.x; i < kSortCap; i += blockDim.x) C.gkeys[i] = lk[i];
@@ -952,19 +1064,24 @@ __global__ __launch_bounds__(kFitThreads) void k_fit(FitArgs A) {
   if (lds_sort) {
     const uint16_t *perm = block_sort_perm<uint16_t>(
         lk, reinterpret_cast<uint16_t *>(dyn_lds + kOffPosA),
-        reinterpret_cast<uint16_t *>(dyn_lds + kOffPosB), m, cnt, run, sm);
+        reinterpret_cast<uint16_t *>(dyn_lds + kOffPosB), m, vary, cnt, run, sm);
     STAMP(3);
     if (cat) fit_categorical<uint16_t>(A, C, sm, H, slot, lk, perm, m);
     else if (m + 1 <= kMixLds) fit_continuous<true, uint16_t>(A, C, sm, H, slot, ob, perm, m, nlt);
     else fit_continuous<false, uint16_t>(A, C, sm, H, slot, ob, perm, m, nlt);
   } else {
-    const uint32_t *perm = block_sort_perm<uint32_t>(C.gkeys, C.gpa, C.gpb, m, cnt, run, sm);
+    const uint32_t *perm =
+        block_sort_perm<uint32_t>(C.gkeys, C.gpa, C.gpb, m, vary, cnt, run, sm);
     STAMP(3);
     if (cat) fit_categorical<uint32_t>(A, C, sm, H, slot, C.gkeys, perm, m);
     else fit_continuous<false, uint32_t>(A, C, sm, H, slot, ob, perm, m, nlt);
   }
   __syncthreads();
   STAMP(10);
+#ifdef TPE_STAMPS
+  if (threadIdx.x == 0 && blockIdx.z == 0)
+    g_stamps[(2 * blockIdx.x + blockIdx.y) & 511][9] = clock64() - clk0;
+#endif
 }
 
 // operator-level split (tpe_split): same threshold, then the mask

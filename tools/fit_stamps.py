@@ -10,7 +10,8 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ['TPE_ENGINE_LIB'] = os.path.join(ROOT, 'hyperopt_amd', 'libtpe_engine_dbg.so')
+os.environ['TPE_ENGINE_LIB'] = os.path.join(
+    ROOT, 'hyperopt_amd', os.environ.get('TPE_STAMPS_LIB', 'libtpe_engine_dbg.so'))
 sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 from hyperopt_amd import _engine as E  # noqa: E402
@@ -30,9 +31,9 @@ def main(cfg, slots):
     for _ in range(3):
         plan.fit()
     eng.lib.tpe_synchronize(eng.h)
-    buf = (C.c_ulonglong * (512 * 16))()
+    buf = (C.c_ulonglong * (512 * 48))()
     assert eng.lib.tpe_debug_stamps(buf) == 0
-    st = np.frombuffer(buf, dtype=np.uint64).reshape(512, 16).astype(np.int64)
+    st = np.frombuffer(buf, dtype=np.uint64).reshape(512, 48).astype(np.int64)
     P = len(dom.space.labels)
     t0 = st[:2 * P, 0].min()
     print(cfg, 'P=%d N=%d' % (P, losses.size))
@@ -44,6 +45,16 @@ def main(cfg, slots):
         print('%-8s %-10s side=%d start=%5.1f ' % (h.label[:8], h.dist[:10], slot % 2,
                                                    (row[0] - t0) / 100.0) + ' '.join(marks))
     print('kernel span: %.1f us' % ((st[:2 * P, 10].max() - t0) / 100.0))
+    sub = {16: 'sd.zero', 17: 'sd.hist', 18: 'sd.bar1', 19: 'sd.scan', 20: 'sd.bar2',
+           21: 'ms.load', 22: 'ms.bitonic64', 23: 'ms.bar', 24: 'ms.L64', 25: 'ms.L128',
+           26: 'ms.L256', 27: 'ms.L512', 28: 'np.plan', 29: 'np.leaves', 30: 'np.end'}
+    for slot in range(min(2 * P, 4)):
+        row = st[slot]
+        print('slot %d last sub-phase stamps (us from slot start): ' % slot + ' '.join(
+            '%s=%.2f' % (nm, (row[i] - row[0]) / 100.0) for i, nm in sub.items() if row[i] >= row[0]))
+    wall = (st[:2 * P, 10] - st[:2 * P, 0]) / 100e6
+    print('shader clock during the fit: %.0f MHz (median over slots)' %
+          np.median(st[:2 * P, 9] / np.maximum(wall, 1e-9) / 1e6))
 
 
 if __name__ == '__main__':
