@@ -18,6 +18,70 @@ __device__ __forceinline__ double np_minimum(double a, double b) {
   return a <= b ? a : b;
 }
 
+// ------------------------------------------------------------------------
+// Cross-lane data movement on DPP (VALU operand modifiers, a few cycles)
+// instead of ds_bpermute (an LDS round trip per step).  Patterns: quad_perm
+// xor 1 / xor 2, row_half_mirror (lane i <- 7 - i in its 8), row_mirror
+// (i <- 15 - i in its 16), row_shr:n, row_bcast:15 / :31 (gfx9 family).
+// ------------------------------------------------------------------------
+enum : int {
+  kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppHalfMirror = 0x141, kDppMirror = 0x140,
+  kDppShr1 = 0x111, kDppShr2 = 0x112, kDppShr4 = 0x114, kDppShr8 = 0x118,
+  kDppBcast15 = 0x142, kDppBcast31 = 0x143
+};
+// lanes without a source (row_shr) or in a disabled row read 0
+template <int CTRL, int ROWS = 0xF>
+__device__ __forceinline__ int dpp(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, ROWS, 0xF, true);
+}
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp64(uint64_t v) {
+  const int lo = dpp<CTRL>((int)(uint32_t)v), hi = dpp<CTRL>((int)(uint32_t)(v >> 32));
+  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+template <int CTRL>
+__device__ __forceinline__ double dppd(double v) {
+  return __builtin_bit_cast(double, dpp64<CTRL>(__builtin_bit_cast(uint64_t, v)));
+}
+// the value of one lane as a wave-uniform scalar
+__device__ __forceinline__ int lane_value(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ uint64_t lane_value64(uint64_t v, int l) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+}
+// wave-wide reductions (every lane must be active); results wave-uniform
+__device__ __forceinline__ int wave_sum(int v) {
+  v += dpp<kDppXor1>(v);
+  v += dpp<kDppXor2>(v);
+  v += dpp<kDppHalfMirror>(v);
+  v += dpp<kDppMirror>(v);  // every lane: its row's sum
+  return lane_value(v, 0) + lane_value(v, 16) + lane_value(v, 32) + lane_value(v, 48);
+}
+__device__ __forceinline__ uint64_t wave_and(uint64_t v) {
+  v &= dpp64<kDppXor1>(v);
+  v &= dpp64<kDppXor2>(v);
+  v &= dpp64<kDppHalfMirror>(v);
+  v &= dpp64<kDppMirror>(v);
+  return lane_value64(v, 0) & lane_value64(v, 16) & lane_value64(v, 32) & lane_value64(v, 48);
+}
+__device__ __forceinline__ uint64_t wave_or(uint64_t v) {
+  v |= dpp64<kDppXor1>(v);
+  v |= dpp64<kDppXor2>(v);
+  v |= dpp64<kDppHalfMirror>(v);
+  v |= dpp64<kDppMirror>(v);
+  return lane_value64(v, 0) | lane_value64(v, 16) | lane_value64(v, 32) | lane_value64(v, 48);
+}
+// inclusive prefix sum over the wave's lanes
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  v += dpp<kDppShr1>(v);
+  v += dpp<kDppShr2>(v);
+  v += dpp<kDppShr4>(v);
+  v += dpp<kDppShr8>(v);
+  v += dpp<kDppBcast15, 0xA>(v);
+  v += dpp<kDppBcast31, 0xC>(v);
+  return v;
+}
+
 // normal_cdf, hyperopt/tpe.py:96-101 (no FMA contraction: bit-level parity).
 __device__ __forceinline__ double normal_cdf(double x, double mu, double sigma) {
 #pragma clang fp contract(off)
@@ -132,14 +196,16 @@ __device__ __forceinline__ void store_lse_envelope(Coef *table, int64_t k, EnvTe
   double lo = valid ? e.m : INFINITY, hi = valid ? e.m : -INFINITY;
   double cm = !valid ? -INFINITY : (e.c == e.c) ? e.c : INFINITY, am = valid ? e.a2 : INFINITY;
   bool bad = valid && (!(e.m == e.m) || !(e.a2 == e.a2));
-#pragma unroll
-  for (int o = 1; o < kCoefBlock; o <<= 1) {
-    lo = fmin(lo, __shfl_xor(lo, o, 64));
-    hi = fmax(hi, __shfl_xor(hi, o, 64));
-    cm = fmax(cm, __shfl_xor(cm, o, 64));
-    am = fmin(am, __shfl_xor(am, o, 64));
-    bad |= __shfl_xor((int)bad, o, 64) != 0;
-  }
+  static_assert(kCoefBlock == 8, "an envelope is one 8-lane DPP group");
+  lo = fmin(lo, dppd<kDppXor1>(lo)); hi = fmax(hi, dppd<kDppXor1>(hi));
+  cm = fmax(cm, dppd<kDppXor1>(cm)); am = fmin(am, dppd<kDppXor1>(am));
+  bad |= dpp<kDppXor1>((int)bad) != 0;
+  lo = fmin(lo, dppd<kDppXor2>(lo)); hi = fmax(hi, dppd<kDppXor2>(hi));
+  cm = fmax(cm, dppd<kDppXor2>(cm)); am = fmin(am, dppd<kDppXor2>(am));
+  bad |= dpp<kDppXor2>((int)bad) != 0;
+  lo = fmin(lo, dppd<kDppHalfMirror>(lo)); hi = fmax(hi, dppd<kDppHalfMirror>(hi));
+  cm = fmax(cm, dppd<kDppHalfMirror>(cm)); am = fmin(am, dppd<kDppHalfMirror>(am));
+  bad |= dpp<kDppHalfMirror>((int)bad) != 0;
   if (k % kCoefBlock) return;
   float *out = reinterpret_cast<float *>(reinterpret_cast<double *>(table) + coef_off(k, 3));
   const float flo = (float)lo, fhi = (float)hi, fc = (float)cm, fa = (float)am;

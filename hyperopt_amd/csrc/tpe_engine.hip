@@ -106,9 +106,11 @@ struct tpe_plan {
     void *stream = nullptr;
     bool table = false;  // below mixtures fit the LDS draw table (kTabCap)
     bool fuse = false;   // ... and the fused k_lattice draw rows' table (kFuseTab)
+    bool small = false;  // k_fit<true> serves the history (fit_small)
     bool operator==(const StepKey &o) const {
       return prior_weight == o.prior_weight && lf == o.lf && n_sug == o.n_sug &&
-             n_cand == o.n_cand && stream == o.stream && table == o.table && fuse == o.fuse;
+             n_cand == o.n_cand && stream == o.stream && table == o.table && fuse == o.fuse &&
+             small == o.small;
     }
   };
   StepKey graph_key, pending_key;
@@ -1197,7 +1199,7 @@ int capture_step(tpe_engine *h, tpe_plan *p, int32_t nb, double prior_weight, in
     if (ty != hipGraphNodeTypeKernel) continue;
     hipKernelNodeParams kp{};
     CKH(hipGraphKernelNodeGetParams(nd, &kp));
-    if (kp.func == fit_kernel_fn()) {
+    if (kp.func == fit_kernel_fn(true) || kp.func == fit_kernel_fn(false)) {
       p->fit_nodes.push_back(nd);
       p->fit_params.push_back(kp);
       p->fit_args0.push_back(*static_cast<const FitArgs *>(kp.kernelParams[0]));
@@ -1280,6 +1282,7 @@ int tpe_plan_fit_suggest(tpe_plan_t p, double gamma, int32_t gamma_cap, double p
   key.stream = (void *)st;
   key.table = (int64_t)nb + 1 <= kTabCap;
   key.fuse = (int64_t)nb + 1 <= kFuseTab;
+  key.small = fit_small(p->n);
   int rc = ensure_suggest_state(h, p, n_sug, 1);
   if (rc) return rc;
   p->h_seeds.assign(seeds, seeds + n_sug);

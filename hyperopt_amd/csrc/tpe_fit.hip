@@ -50,6 +50,7 @@ constexpr int kSortCap = 10000;              // elements sorted in LDS (u16 posi
 constexpr int kMixLds = 4097;                // K kept in LDS until copy-out (m <= 4096)
 constexpr int kMixStride = 4104;             // doubles per LDS mixture array
 constexpr int kDigits = 256;
+constexpr int kPreN = 4 * kFitThreads;       // histories held in registers by k_fit
 
 // dynamic LDS map (bytes)
 constexpr int kOffKeys = 0;                               // u64 [kSortCap]
@@ -60,23 +61,38 @@ constexpr int kOffRun = kOffCnt + 4 * kDigits * kFitWaves;  // u32 [16][256]
 constexpr int kFitLds = kOffRun + 4 * kDigits * kFitWaves;  // 155,648 B
 static_assert(4 * 8 * kMixStride <= kFitLds, "LDS mixture arrays");
 
-// numpy pairwise_sum tree of one chunk length n (<= 8192): leaves of <= 128
-// elements, internal node = left + right with left = floor(n/2) rounded down
-// to a multiple of 8.  Built breadth-first by one wave (lanes = nodes of a
-// level) and evaluated bottom-up level by level by one wave, so neither the
-// planning nor the combine is a serial recursion.
-constexpr int kNpNodes = 2 * kMaxLeaves;
-struct NpPlan {
-  int n, n_leaves, n_int, levels;
-  uint16_t leaf_lo[kMaxLeaves], leaf_n[kMaxLeaves], leaf_id[kMaxLeaves];
-  uint16_t int_lo[kMaxLeaves], int_n[kMaxLeaves], int_id[kMaxLeaves], int_cid[kMaxLeaves];
-  uint16_t lvl_begin[16];  // internal nodes of level d: [lvl_begin[d], lvl_begin[d + 1])
+// numpy pairwise_sum tree of one chunk (n <= 8192): a node of length m > 128
+// splits into m2 = floor(m/2) rounded down to a multiple of 8 and m - m2, a
+// node of <= 128 is a leaf.  A child is at most half its parent + 8, so the
+// tree is at most 7 levels deep and its nodes fit a 1-based heap of 256 ids
+// (children of id: 2 id, 2 id + 1).  Any thread finds a node's range from its
+// id by descending from the root, so no tree has to be built first.
+constexpr int kNpHeap = 256;
+
+struct NpNode {
+  int lo, n;  // n = 0: no such node (an ancestor is a leaf)
+};
+__device__ __forceinline__ NpNode np_node(int len, int id) {
+  const int depth = 31 - __builtin_clz((unsigned)id);
+  int lo = 0, n = len;
+  for (int b = depth - 1; b >= 0; --b) {
+    if (n <= 128) return NpNode{0, 0};
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    if ((id >> b) & 1) { lo += n2; n -= n2; }
+    else n = n2;
+  }
+  return NpNode{lo, n};
+}
+
+struct GatherEx {  // one wave's share of a gather chunk
+  int cnt, nlt;
+  uint64_t kand, kor;
 };
 
 struct FitShared {
-  NpPlan np;                 // pairwise-sum tree of the last chunk length
-  double val[2][kNpNodes];   // node sums (two arrays summed together)
-  double total2[2];
+  GatherEx gx[2][kFitWaves];
+  double val[2][kNpHeap];    // pairwise-sum node values by heap id (two arrays at once)
   uint64_t rk[2][kFitWaves];
   uint32_t rp[2][kFitWaves];
   uint64_t vand[kFitWaves], vor[kFitWaves];
@@ -98,26 +114,14 @@ __device__ __forceinline__ void wave_min_kp(uint64_t &k, uint32_t &p) {
 }
 
 __device__ __forceinline__ uint32_t wave_excl_scan_u32(uint32_t v) {
-  const int lane = threadIdx.x & 63;
-  uint32_t x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
-  return x - v;
+  return (uint32_t)wave_incl_scan((int)v) - v;
 }
 
 // block-wide exclusive scan of small ints: (exclusive prefix, total) -- by
 // value, in registers (an out-reference of a call lives on the scratch stack)
-__device__ NOINLINE int2 block_excl_scan(int v, int *wsum) {
+__device__ __forceinline__ int2 block_excl_scan(int v, int *wsum) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  int x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
+  const int x = wave_incl_scan(v);
   if (lane == 63) wsum[w] = x;
   __syncthreads();
   int before = 0, tot = 0;
@@ -271,20 +275,42 @@ __device__ void merge_sort_1024(const uint64_t *keys, int n, uint16_t *out, uint
 // is dropped (!lossy); otherwise a run of equal truncated keys is ordered by
 // position, so each such run (rare, short) is re-ranked by its full keys;
 // false (the caller then sorts the full keys) for a run of more than kRunMax.
-__device__ void wave_bitonic64_packed(uint64_t &k) {
-  const int lane = threadIdx.x & 63;
-  for (int kk = 2; kk <= 64; kk <<= 1) {
-    for (int j = kk >> 1; j > 0; j >>= 1) {
-      const bool asc = (lane & kk) == 0 || kk == 64;
-      const uint64_t ok = __shfl_xor(k, j, 64);
-      const bool lower = (lane & j) == 0;
-      const bool other_less = ok < k;
-      if ((lower == asc) ? other_less : !other_less) k = ok;
-    }
+// the word of lane ^ J: DPP for J < 16 (row_shl / row_shr pairs for 4 and 8),
+// ds_bpermute across rows
+template <int J>
+__device__ __forceinline__ uint64_t xor_lane64(uint64_t v) {
+  if constexpr (J == 1) return dpp64<kDppXor1>(v);
+  else if constexpr (J == 2) return dpp64<kDppXor2>(v);
+  else if constexpr (J == 4 || J == 8) {
+    const uint64_t up = dpp64<0x100 + J>(v);  // row_shl:J  (lane + J)
+    const uint64_t dn = dpp64<0x110 + J>(v);  // row_shr:J  (lane - J)
+    return (threadIdx.x & J) ? dn : up;
+  } else {
+    return __shfl_xor(v, J, 64);
   }
 }
+template <int KK, int J>
+__device__ __forceinline__ void bitonic_stage(uint64_t &k) {
+  const int lane = threadIdx.x & 63;
+  const bool asc = (lane & KK) == 0 || KK == 64;
+  const uint64_t ok = xor_lane64<J>(k);
+  const bool lower = (lane & J) == 0;
+  const bool other_less = ok < k;
+  if ((lower == asc) ? other_less : !other_less) k = ok;
+}
+__device__ __forceinline__ void wave_bitonic64_packed(uint64_t &k) {
+  bitonic_stage<2, 1>(k);
+  bitonic_stage<4, 2>(k); bitonic_stage<4, 1>(k);
+  bitonic_stage<8, 4>(k); bitonic_stage<8, 2>(k); bitonic_stage<8, 1>(k);
+  bitonic_stage<16, 8>(k); bitonic_stage<16, 4>(k); bitonic_stage<16, 2>(k);
+  bitonic_stage<16, 1>(k);
+  bitonic_stage<32, 16>(k); bitonic_stage<32, 8>(k); bitonic_stage<32, 4>(k);
+  bitonic_stage<32, 2>(k); bitonic_stage<32, 1>(k);
+  bitonic_stage<64, 32>(k); bitonic_stage<64, 16>(k); bitonic_stage<64, 8>(k);
+  bitonic_stage<64, 4>(k); bitonic_stage<64, 2>(k); bitonic_stage<64, 1>(k);
+}
 
-__device__ bool merge_sort_1024_packed(const uint64_t *keys, int n, int shift, bool lossy,
+__device__ __forceinline__ bool merge_sort_1024_packed(const uint64_t *keys, int n, int shift, bool lossy,
                                        uint16_t *out, uint64_t *b0, uint64_t *b1) {
   const int t = threadIdx.x;
   // padding (t >= n): all-ones key bits, position t > every real position
@@ -292,17 +318,28 @@ __device__ bool merge_sort_1024_packed(const uint64_t *keys, int n, int shift, b
   wave_bitonic64_packed(k);
   b0[t] = k;
   __syncthreads();
+  // two 4-way merge levels (64 -> 256 -> 1024): an element's position in its
+  // quad of runs is its index in its own run plus its rank in each of the
+  // three others (all words distinct), three branch-free binary searches
+  // side by side -- half the dependent LDS reads of four pairwise levels
+  static_assert(kFitThreads == 1024, "64 * 4 * 4");
   uint64_t *sk = b0, *dk = b1;
-  for (int len = 64; len < kFitThreads; len <<= 1) {
-    const int run = t / len, idx = t % len;
-    const int other = (run ^ 1) * len;
-    int lo = 0, hi = len;  // lower bound of k in the partner run (all words distinct)
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (sk[other + mid] < k) lo = mid + 1;
-      else hi = mid;
+#pragma unroll
+  for (int len = 64; len < kFitThreads; len <<= 2) {
+    const int qb = t & ~(4 * len - 1), r = (t / len) & 3;
+    const uint64_t *o1 = sk + qb + ((r + 1) & 3) * len, *o2 = sk + qb + ((r + 2) & 3) * len,
+                   *o3 = sk + qb + ((r + 3) & 3) * len;
+    int i1 = 0, i2 = 0, i3 = 0;
+#pragma unroll
+    for (int step = len / 2; step > 0; step >>= 1) {
+      i1 += (o1[i1 + step - 1] < k) ? step : 0;
+      i2 += (o2[i2 + step - 1] < k) ? step : 0;
+      i3 += (o3[i3 + step - 1] < k) ? step : 0;
     }
-    dk[(run & ~1) * len + idx + lo] = k;
+    i1 += (o1[i1] < k) ? 1 : 0;
+    i2 += (o2[i2] < k) ? 1 : 0;
+    i3 += (o3[i3] < k) ? 1 : 0;
+    dk[qb + (t & (len - 1)) + i1 + i2 + i3] = k;
     __syncthreads();
     uint64_t *tk = sk; sk = dk; dk = tk;
     k = sk[t];  // this thread now owns merged position t
@@ -336,8 +373,8 @@ __device__ bool merge_sort_1024_packed(const uint64_t *keys, int n, int shift, b
   return !__syncthreads_or(bad);
 }
 
-template <typename PosT>
-__device__ PosT *block_sort_perm(const uint64_t *keys, PosT *a, PosT *b, int n, uint64_t vary,
+template <typename PosT, bool SMALL = false>
+__device__ __forceinline__ PosT *block_sort_perm(const uint64_t *keys, PosT *a, PosT *b, int n, uint64_t vary,
                                  uint32_t *cnt, uint32_t *run, FitShared &sm) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (n > 64 && n <= kMergeMax && sizeof(PosT) == 2) {
@@ -364,6 +401,7 @@ __device__ PosT *block_sort_perm(const uint64_t *keys, PosT *a, PosT *b, int n, 
     __syncthreads();
     return a;
   }
+  if (SMALL) return a;  // n <= kMergeMax: unreachable
   for (int i = threadIdx.x; i < n; i += blockDim.x) a[i] = (PosT)i;
   __syncthreads();
   for (int shift = 0; shift < 64; shift += 8) {
@@ -375,111 +413,27 @@ __device__ PosT *block_sort_perm(const uint64_t *keys, PosT *a, PosT *b, int n, 
 }
 
 // ------------------------------------------------------------------------
-// numpy float64 sum (ndarray.sum): buffers of 8192 elements, each reduced by
-// pairwise_sum (leaves of <= 128 with 8 accumulators, split at n/2 rounded
-// down to a multiple of 8), buffer results added in order.  Leaves run in
-// parallel on 8-lane groups, lane s owning numpy's accumulator r[s].
-// ------------------------------------------------------------------------
-// wave 0: breadth-first construction of the tree of length n
-__device__ NOINLINE void np_plan(int n, NpPlan &P) {
-  const int lane = threadIdx.x & 63;
-  int nl = 0, ni = 0, next_id = 1, lvl = 0;
-  // root
-  if (n <= 128) {
-    if (lane == 0) { P.leaf_lo[0] = 0; P.leaf_n[0] = (uint16_t)n; P.leaf_id[0] = 0; }
-    nl = 1;
-  } else {
-    if (lane == 0) { P.int_lo[0] = 0; P.int_n[0] = (uint16_t)n; P.int_id[0] = 0; P.lvl_begin[0] = 0; }
-    ni = 1;
-  }
-  int b0 = 0, b1 = ni;  // internal nodes of the current level
-  while (b1 > b0) {
-    if (lane == 0) P.lvl_begin[lvl] = (uint16_t)b0;
-    // children of this level's internal nodes, in order; 4 parents per lane max
-    int add_l = 0, add_i = 0;
-    for (int c0 = b0; c0 < b1; c0 += 64) {
-      const int c = c0 + lane;
-      const bool v = c < b1;
-      int off = 0, m = 0;
-      if (v) { off = P.int_lo[c]; m = P.int_n[c]; }
-      int n2 = m / 2;
-      n2 -= n2 % 8;
-      const int cl_off = off, cl_n = n2, cr_off = off + n2, cr_n = m - n2;
-      const bool lleaf = v && cl_n <= 128, rleaf = v && cr_n <= 128;
-      const bool lint = v && !lleaf, rint = v && !rleaf;
-      // child ids: 2 per parent, in parent order (left, right)
-      const int my_ids = v ? 2 : 0;
-      const int id_base = next_id + (int)wave_excl_scan_u32((uint32_t)my_ids);
-      const int lp = (int)wave_excl_scan_u32((uint32_t)(lleaf + rleaf));
-      const int ip = (int)wave_excl_scan_u32((uint32_t)(lint + rint));
-      int li = nl + add_l + lp, ii = b1 + add_i + ip;
-      if (v) {
-        const int idl = id_base, idr = id_base + 1;
-        P.int_cid[c] = (uint16_t)idl;
-        // left child first, then right (order inside a level is free)
-        if (lleaf) { P.leaf_lo[li] = cl_off; P.leaf_n[li] = cl_n; P.leaf_id[li] = idl; ++li; }
-        else { P.int_lo[ii] = cl_off; P.int_n[ii] = cl_n; P.int_id[ii] = idl; ++ii; }
-        if (rleaf) { P.leaf_lo[li] = cr_off; P.leaf_n[li] = cr_n; P.leaf_id[li] = idr; }
-        else { P.int_lo[ii] = cr_off; P.int_n[ii] = cr_n; P.int_id[ii] = idr; }
-      }
-      // totals of this 64-parent batch (lane 63 holds the last prefix)
-      const int last = min(64, b1 - c0) - 1;
-      const int tl = __shfl(lp + (int)(lleaf + rleaf), last, 64);
-      const int ti = __shfl(ip + (int)(lint + rint), last, 64);
-      const int tid = __shfl(id_base + my_ids, last, 64) - next_id;
-      add_l += tl;
-      add_i += ti;
-      next_id += tid;
-    }
-    nl += add_l;
-    b0 = b1;
-    b1 = b1 + add_i;
-    ++lvl;
-  }
-  if (lane == 0) {
-    P.n = n; P.n_leaves = nl; P.n_int = b1; P.levels = lvl; P.lvl_begin[lvl] = (uint16_t)b1;
-  }
-}
-
-// wave 0: bottom-up evaluation of the tree (node = left + right)
-template <int NA>
-__device__ __forceinline__ void np_combine_wave(const NpPlan &P, double (&val)[2][kNpNodes]) {
-  const int lane = threadIdx.x & 63;
-  for (int l = P.levels - 1; l >= 0; --l) {
-    const int c1 = P.lvl_begin[l + 1];
-    for (int c = P.lvl_begin[l] + lane; c < c1; c += 64) {
-      const int id = P.int_id[c], cid = P.int_cid[c];
-#pragma unroll
-      for (int q = 0; q < NA; ++q) val[q][id] = val[q][cid] + val[q][cid + 1];
-    }
-    // LDS ops of one wave complete in order: the next level reads these
-  }
-}
-
 // numpy float64 sum (ndarray.sum) of NA arrays: buffers of 8192 elements,
-// each by the pairwise tree above, buffer results added in order.  Leaves
-// run in parallel on 8-lane groups, lane s owning numpy's accumulator r[s].
+// each reduced by the pairwise tree above, buffer results added in order.
+// Leaves run in parallel on 8-lane groups, lane s owning numpy's accumulator
+// r[s]; wave 0 then adds the internal nodes level by level (a wave's LDS ops
+// complete in order, so the levels need no barrier).
 template <int NA>
 __device__ __forceinline__ void block_np_sums(const double *const (&arr)[NA], int64_t n,
                                               FitShared &sm, double (&out)[NA]) {
   const int s = threadIdx.x & 7, groups = blockDim.x >> 3;
-  NpPlan &P = sm.np;
   for (int64_t c0 = 0; c0 < n; c0 += 8192) {
     const int cn = (int)min<int64_t>(8192, n - c0);
-    __syncthreads();
-    if (threadIdx.x < 64 && P.n != cn) np_plan(cn, P);
-    __syncthreads();
-    STAMP(28);
-    const int nl = P.n_leaves;
-    for (int g0 = 0; g0 < nl; g0 += groups) {  // uniform trip count
-      const int g = g0 + (threadIdx.x >> 3);
-      const bool has = g < nl;
-      const int ln = has ? P.leaf_n[g] : 0;
-      const int off = (int)c0 + (has ? P.leaf_lo[g] : 0);
+    __syncthreads();  // previous chunk's root consumed, the arrays written
+    for (int id0 = 1; id0 < kNpHeap; id0 += groups) {  // uniform trip count
+      const int id = id0 + (threadIdx.x >> 3);
+      const NpNode nd = id < kNpHeap ? np_node(cn, id) : NpNode{0, 0};
+      const bool leaf = nd.n > 0 && nd.n <= 128;
+      const int ln = leaf ? nd.n : 0;
       const int body = ln - ln % 8;
 #pragma unroll
       for (int q = 0; q < NA; ++q) {
-        const double *p = arr[q] + off;
+        const double *p = arr[q] + c0 + nd.lo;
         double r = 0.0;
         if (ln >= 8) {
           r = p[s];
@@ -487,10 +441,13 @@ __device__ __forceinline__ void block_np_sums(const double *const (&arr)[NA], in
 #pragma unroll 4
           for (int i = 8 + s; i < body; i += 8) r += p[i];
         }
-        r = r + __shfl_xor(r, 1, 64);
-        r = r + __shfl_xor(r, 2, 64);
-        r = r + __shfl_xor(r, 4, 64);
-        if (has && s == 0) {
+        // ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)) in lane s = 0
+        // (fp addition commutes exactly; half_mirror brings lane 7's
+        // (r6 + r7) + (r4 + r5) to lane 0)
+        r = r + dppd<kDppXor1>(r);
+        r = r + dppd<kDppXor2>(r);
+        r = r + dppd<kDppHalfMirror>(r);
+        if (leaf && s == 0) {
           double res;
           if (ln < 8) {
             res = 0.0;
@@ -499,26 +456,33 @@ __device__ __forceinline__ void block_np_sums(const double *const (&arr)[NA], in
             res = r;
             for (int i = body; i < ln; ++i) res += p[i];
           }
-          sm.val[q][P.leaf_id[g]] = res;
+          sm.val[q][id] = res;
         }
       }
     }
     __syncthreads();
-    STAMP(29);
     if (threadIdx.x < 64) {
-      np_combine_wave<NA>(P, sm.val);
-      if (threadIdx.x == 0) {
+      const int lane = threadIdx.x;
+      for (int d = 6; d >= 0; --d) {  // internal nodes live at depth <= 6
+        const int id = (1 << d) + lane;
+        if (lane < (1 << d) && np_node(cn, id).n > 128) {
+#pragma unroll
+          for (int q = 0; q < NA; ++q) sm.val[q][id] = sm.val[q][2 * id] + sm.val[q][2 * id + 1];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      }
+      // running total of the buffers in the unused heap slot 0
+      if (lane == 0) {
 #pragma unroll
         for (int q = 0; q < NA; ++q)
-          sm.total2[q] = (c0 == 0) ? (0.0 + sm.val[q][0]) : (sm.total2[q] + sm.val[q][0]);
+          sm.val[q][0] = (c0 == 0) ? (0.0 + sm.val[q][1]) : (sm.val[q][0] + sm.val[q][1]);
       }
     }
   }
   __syncthreads();
   STAMP(30);
 #pragma unroll
-  for (int q = 0; q < NA; ++q) out[q] = n > 0 ? sm.total2[q] : 0.0;
-  __syncthreads();
+  for (int q = 0; q < NA; ++q) out[q] = n > 0 ? sm.val[q][0] : 0.0;
 }
 
 __device__ double block_np_sum(const double *a, int64_t n, FitShared &sm) {
@@ -552,13 +516,17 @@ __device__ __forceinline__ double lf_weight(const LfRamp &r, int64_t i) {
   return (double)i * r.step + r.start;
 }
 
-__device__ __forceinline__ double obs_transform(double v, int32_t tf, double low) {
-  switch (tf) {
-    case TPE_OBS_LOG: return log(v);
-    case TPE_OBS_LOG_CLIP_EXPLOW: return log(np_maximum(v, np_maximum(kEPS, exp(low))));
-    case TPE_OBS_LOG_CLIP_EPS: return log(np_maximum(v, kEPS));
-    default: return v;
-  }
+// the observation transform of an hp (tpe.py:510-560 posteriors): one log
+// at most per value; `floor` = the clip's lower bound (max(EPS, exp(low)) or
+// EPS), computed once per slot by ObsFloor
+__device__ __forceinline__ double obs_floor(int32_t tf, double low) {
+  if (tf == TPE_OBS_LOG_CLIP_EXPLOW) return np_maximum(kEPS, exp(low));
+  return kEPS;
+}
+__device__ __forceinline__ double obs_transform(double v, int32_t tf, double floor) {
+  if (tf == TPE_OBS_IDENT) return v;
+  const bool clip = tf == TPE_OBS_LOG_CLIP_EXPLOW || tf == TPE_OBS_LOG_CLIP_EPS;
+  return log(clip ? np_maximum(v, floor) : v);
 }
 
 // ------------------------------------------------------------------------
@@ -605,7 +573,7 @@ struct TiedPosAt {  // positions of the trials whose key equals T
 // `prefix`, then the digit holding the need-th (1-based) smallest; `need`
 // becomes the rank inside that digit.
 template <typename ValFn>
-__device__ NOINLINE Digit select_digit(ValFn val, int n, uint64_t mask, uint64_t prefix, int shift,
+__device__ __forceinline__ Digit select_digit(ValFn val, int n, uint64_t mask, uint64_t prefix, int shift,
                                        uint32_t need, uint32_t *hist, FitShared &sm, int par) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   // hist[0..256) is zero on entry; zero the other half for the next step
@@ -651,7 +619,11 @@ __device__ NOINLINE Digit select_digit(ValFn val, int n, uint64_t mask, uint64_t
 // (a2) the n_below-th smallest (loss key, position) by radix select over the
 // 64-bit keys (digits constant over all losses skipped), then -- only when
 // several trials tie on that loss -- over the positions of the tied ones.
-__device__ Split compute_split(const FitArgs &A, const FitCtx &C, FitShared &sm) {
+// pre: the block holds the history in registers (n <= kPreN, trials
+// 4 t .. 4 t + 3 of thread t, see Prefetch); otherwise losses are read here.
+template <bool SMALL = false>
+__device__ __forceinline__ Split compute_split(const FitArgs &A, const FitCtx &C, FitShared &sm,
+                                               bool pre, const double (&pls)[4]) {
   const int n = (int)A.n;
   const int nb = A.n_below;
   if (nb <= 0 || n == 0) return Split{0, 0, 0};
@@ -659,22 +631,37 @@ __device__ Split compute_split(const FitArgs &A, const FitCtx &C, FitShared &sm)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   uint64_t *lk = reinterpret_cast<uint64_t *>(C.lds + kOffKeys);
   uint32_t *hist = reinterpret_cast<uint32_t *>(C.lds + kOffCnt);
-  uint64_t *keys = n <= kSortCap ? lk : C.gkeys;
+  uint64_t *keys = (SMALL || n <= kSortCap) ? lk : C.gkeys;
   for (int d = threadIdx.x; d < kDigits; d += blockDim.x) hist[d] = 0;
+  STAMP(31);
   uint64_t an = ~0ull, on = 0ull;
-  for (int j = threadIdx.x; j < n; j += blockDim.x) {
-    const uint64_t k = sort_key(A.losses[j]);
-    keys[j] = k;
-    an &= k;
-    on |= k;
-  }
+  if (pre) {
+    constexpr int PER = SMALL ? 1 : 4;  // trials per thread in registers
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    an &= __shfl_xor(an, o, 64);
-    on |= __shfl_xor(on, o, 64);
+    for (int u = 0; u < PER; ++u) {
+      const int j = PER * threadIdx.x + u;
+      if (j < n) {
+        const uint64_t k = sort_key(pls[u]);
+        lk[j] = k;
+        an &= k;
+        on |= k;
+      }
+    }
+  } else {
+    for (int j = threadIdx.x; j < n; j += blockDim.x) {
+      const uint64_t k = sort_key(A.losses[j]);
+      keys[j] = k;
+      an &= k;
+      on |= k;
+    }
   }
+  STAMP(32);
+  an = wave_and(an);
+  on = wave_or(on);
   if (lane == 0) { sm.vand[w] = an; sm.vor[w] = on; }
+  STAMP(33);
   __syncthreads();
+  STAMP(34);
   an = ~0ull;
   on = 0ull;
 #pragma unroll
@@ -722,7 +709,7 @@ __device__ Split compute_split(const FitArgs &A, const FitCtx &C, FitShared &sm)
 // reduction per 8 components, computed with the coefficients) and the
 // padding components of the last block (alpha = -inf: terms exactly 0).
 // ------------------------------------------------------------------------
-__device__ void store_table(const tpe_hp &H, Coef *cf, int K, const double *w, const double *mu,
+__device__ __forceinline__ void store_table(const tpe_hp &H, Coef *cf, int K, const double *w, const double *mu,
                             const double *sg, double pacc, bool quant) {
   const int kp = (K + kCoefBlock - 1) / kCoefBlock * kCoefBlock;
   // kp and the block size are multiples of 8: the 8 lanes of a block's
@@ -741,9 +728,12 @@ __device__ void store_table(const tpe_hp &H, Coef *cf, int K, const double *w, c
 // per-component lpdf constants + truncation mass of one slot (block-wide);
 // w/mu/sg may be LDS or global; tmp: K doubles of scratch
 // ------------------------------------------------------------------------
-__device__ void prep_slot(const tpe_hp &H, int64_t slot, int K, const double *w, const double *mu,
+// (the descriptor comes by global pointer: a reference to a by-value copy
+// would put that copy on the scratch stack when the call is not inlined)
+__device__ __forceinline__ void prep_slot(const tpe_hp *Hg, int64_t slot, int K, const double *w, const double *mu,
                           const double *sg, MixInfo *info, Coef *coef, int64_t kcap, double *tmp,
                           FitShared &sm) {
+  const tpe_hp H = *Hg;
   Coef *cf = coef + slot * kcap;
   const double wsum = block_np_sum(w, K, sm);
   STAMP(7);
@@ -784,8 +774,8 @@ __device__ void prep_slot(const tpe_hp &H, int64_t slot, int K, const double *w,
 // (a4) adaptive_parzen_normal on the m observations ob[] (tid order) after
 // the sort; nlt = #{obs < prior_mu} = searchsorted(sorted, prior_mu, 'left')
 // ------------------------------------------------------------------------
-template <bool MIXLDS, typename PosT>
-__device__ void fit_continuous(const FitArgs &A, const FitCtx &C, FitShared &sm, const tpe_hp &H,
+template <bool MIXLDS, typename PosT, int QN = 4>  // QN: observations per thread (m <= QN * 1024)
+__device__ __forceinline__ void fit_continuous(const FitArgs &A, const FitCtx &C, FitShared &sm, const tpe_hp &H,
                                int64_t slot, const double *ob, const PosT *perm, int m, int nlt) {
   const double pm = H.prior_mu, ps = H.prior_sigma;
   const int K = m + 1;
@@ -805,7 +795,7 @@ __device__ void fit_continuous(const FitArgs &A, const FitCtx &C, FitShared &sm,
   if (MIXLDS) {
     double v[4], wt[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < QN; ++q) {
       const int r = threadIdx.x + q * kFitThreads;
       if (r < m) {
         const int e = (int)perm[r];
@@ -815,7 +805,7 @@ __device__ void fit_continuous(const FitArgs &A, const FitCtx &C, FitShared &sm,
     }
     __syncthreads();  // perm (LDS) is overwritten by the mixture arrays below
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < QN; ++q) {
       const int r = threadIdx.x + q * kFitThreads;
       if (r < m) {
         const int o = r + (r >= pos ? 1 : 0);
@@ -891,7 +881,7 @@ __device__ void fit_continuous(const FitArgs &A, const FitCtx &C, FitShared &sm,
 // serial sum keeps the reference's rounding.
 // ------------------------------------------------------------------------
 template <typename PosT>
-__device__ void fit_categorical(const FitArgs &A, const FitCtx &C, FitShared &sm,
+__device__ __forceinline__ void fit_categorical(const FitArgs &A, const FitCtx &C, FitShared &sm,
                                 const tpe_hp &H, int64_t slot, const uint64_t *keys,
                                 const PosT *perm, int m) {
   const int upper = H.upper;
@@ -942,7 +932,7 @@ __device__ void fit_categorical(const FitArgs &A, const FitCtx &C, FitShared &sm
     sg[c] = 0.0;
   }
   __syncthreads();
-  prep_slot(H, slot, upper, w, mu, sg, A.info, A.coef, A.kcap, A.tmp + slot * A.kcap, sm);
+  prep_slot(A.hps + slot / 2, slot, upper, w, mu, sg, A.info, A.coef, A.kcap, A.tmp + slot * A.kcap, sm);
 }
 
 // ------------------------------------------------------------------------
@@ -951,24 +941,29 @@ __device__ void fit_categorical(const FitArgs &A, const FitCtx &C, FitShared &sm
 #ifndef TPE_FIT_REPS
 #define TPE_FIT_REPS 1  // diagnostic builds: > 1 repeats the fit (warm caches)
 #endif
+template <bool SMALL>
 __device__ __forceinline__ void fit_slot(const FitArgs &A, unsigned char *dyn_lds,
                                          FitShared &sm);
 
+// SMALL: histories of <= kMergeMax trials, the whole fit in LDS; a separate
+// instantiation without the large-history paths keeps the code a CU pair
+// runs (and shares one instruction cache for) small
+template <bool SMALL>
 __global__ __launch_bounds__(kFitThreads) void k_fit(FitArgs A) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn_lds[];
   __shared__ FitShared sm;
   for (int rep = 0; rep < TPE_FIT_REPS; ++rep) {
-    fit_slot(A, dyn_lds, sm);
+    fit_slot<SMALL>(A, dyn_lds, sm);
     __syncthreads();
   }
 }
 
+template <bool SMALL>
 __device__ __forceinline__ void fit_slot(const FitArgs &A, unsigned char *dyn_lds,
                                          FitShared &sm) {
   const int hp = blockIdx.x, side = blockIdx.y;  // side 0 = below ("good")
   const int64_t slot = 2 * (int64_t)hp + side;
   const tpe_hp H = A.hps[hp];
-  if (threadIdx.x == 0) sm.np.n = -1;
   FitCtx C;
   C.lds = dyn_lds;
   unsigned char *gsb = A.sortbuf + slot * 16 * A.scap;
@@ -979,97 +974,132 @@ __device__ __forceinline__ void fit_slot(const FitArgs &A, unsigned char *dyn_ld
 #ifdef TPE_STAMPS
   const unsigned long long clk0 = clock64();  // shader clock: SCLK = cycles / wall time
 #endif
-  const Split t = compute_split(A, C, sm);
+  // small histories: every trial's (loss, value, activity) is loaded into
+  // registers up front, so the gather below needs no second memory round trip
+  const bool pre = SMALL || A.n <= kPreN;
+  constexpr int PER = SMALL ? 1 : 4;  // consecutive trials per thread (gather, prefetch)
+  const double *row = A.vals + (int64_t)hp * A.ld;
+  const uint8_t *arow = A.active + (int64_t)hp * A.ld;
+  double pls[4] = {0.0, 0.0, 0.0, 0.0}, prv[4] = {0.0, 0.0, 0.0, 0.0};
+  uint8_t pac[4] = {0, 0, 0, 0};
+  if (pre) {
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int64_t j = min<int64_t>(PER * (int64_t)threadIdx.x + u, A.n - 1);
+      pac[u] = j >= 0 ? arow[j] : 0;
+      pls[u] = j >= 0 ? A.losses[j] : 0.0;
+      prv[u] = j >= 0 ? row[j] : 0.0;
+    }
+  }
+  const Split t = compute_split<SMALL>(A, C, sm, pre, pls);
   __syncthreads();
   STAMP(1);
 
   // ---- gather this side's observations in tid order (tpe.py:629-636):
   // 4 consecutive trials per thread, one block scan per 4096 trials
   const bool cat = H.family == TPE_CAT;
-  const double *row = A.vals + (int64_t)hp * A.ld;
-  const uint8_t *arow = A.active + (int64_t)hp * A.ld;
   // observations: LDS above the keys when the history is small (no global
   // stores in flight at the barriers that follow), else slot scratch
-  double *ob = A.n <= kMergeMax
+  double *ob = (SMALL || A.n <= kMergeMax)
                    ? reinterpret_cast<double *>(dyn_lds + kOffKeys + 8 * kMergeMax)
                    : A.ob + slot * A.kcap;
   uint64_t *lk = reinterpret_cast<uint64_t *>(dyn_lds + kOffKeys);
   int m = 0, nlt = 0;
   uint64_t kand = ~0ull, kor = 0ull;  // bits equal over all keys: kand == kor there
-  for (int64_t c0 = 0; c0 < A.n; c0 += 4 * kFitThreads) {
-    const int64_t j0 = c0 + 4 * (int64_t)threadIdx.x;
+  const double ofloor = obs_floor(H.obs_transform, H.low);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int chunk = 0;
+  for (int64_t c0 = 0; c0 < A.n; c0 += PER * kFitThreads, ++chunk) {
+    const int64_t j0 = c0 + PER * (int64_t)threadIdx.x;
     bool f[4];
     double v[4];
     int cntl = 0;
     // all loads issued before any use: one memory round trip per chunk
     uint8_t ac[4];
     double ls[4], rv[4];
+    if (pre) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int64_t j = min<int64_t>(j0 + u, A.n - 1);
-      ac[u] = arow[j];
-      ls[u] = A.losses[j];
-      rv[u] = row[j];
+      for (int u = 0; u < PER; ++u) { ac[u] = pac[u]; ls[u] = pls[u]; rv[u] = prv[u]; }
+    } else {
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int64_t j = min<int64_t>(j0 + u, A.n - 1);
+        ac[u] = arow[j];
+        ls[u] = A.losses[j];
+        rv[u] = row[j];
+      }
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < PER; ++u) {
       const int64_t j = j0 + u;
       f[u] = j < A.n && ac[u] && (is_below(t, sort_key(ls[u]), (uint32_t)j) == (side == 0));
       v[u] = 0.0;
       if (f[u]) {
-        v[u] = obs_transform(rv[u], H.obs_transform, H.low);
+        v[u] = obs_transform(rv[u], H.obs_transform, ofloor);
         nlt += (v[u] < H.prior_mu) ? 1 : 0;
+        const uint64_t k = cat ? (uint64_t)(int64_t)v[u] : sort_key(v[u]);
+        kand &= k;
+        kor |= k;
       }
       cntl += f[u] ? 1 : 0;
     }
-    const int2 sc = block_excl_scan(cntl, sm.wsum);
-    const int tot = sc.y;
-    int i = m + sc.x;
+    STAMP(35);
+    // one exchange per chunk (double-buffered by chunk parity, so a single
+    // barrier): the wave's count for the scan, and the running nlt / key-bit
+    // reductions, which are final after the last chunk
+    const int x = wave_incl_scan(cntl);
+    const int nw = wave_sum(nlt);
+    const uint64_t aw = wave_and(kand), ow = wave_or(kor);
+    GatherEx &ex = sm.gx[chunk & 1][wv];
+    if (lane == 63) { ex.cnt = x; ex.nlt = nw; ex.kand = aw; ex.kor = ow; }
+    __syncthreads();
+    int before = 0, tot = 0, nl = 0;
+    uint64_t ka = ~0ull, ko = 0ull;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int i = 0; i < kFitWaves; ++i) {
+      const GatherEx &e = sm.gx[chunk & 1][i];
+      before += (i < wv) ? e.cnt : 0;
+      tot += e.cnt;
+      nl += e.nlt;
+      ka &= e.kand;
+      ko |= e.kor;
+    }
+    STAMP(36);
+    int i = m + before + x - cntl;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
       if (!f[u]) continue;
       ob[i] = v[u];
-      const uint64_t k = cat ? (uint64_t)(int64_t)v[u] : sort_key(v[u]);
-      kand &= k;
-      kor |= k;
+      const uint64_t k = cat ? (uint64_t)(int64_t)v[u] : sort_key(v[u]);  // (recomputed: registers)
       if (i < kSortCap) lk[i] = k;
       else C.gkeys[i] = k;
       ++i;
     }
     m += tot;
+    if (c0 + PER * kFitThreads >= A.n) { nlt = nl; kand = ka; kor = ko; }  // block totals
   }
-  {  // block reductions: nlt, and the varying key bits for the sort
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      nlt += __shfl_xor(nlt, o, 64);
-      kand &= __shfl_xor(kand, o, 64);
-      kor |= __shfl_xor(kor, o, 64);
-    }
-    if (lane == 0) { sm.isum[w] = nlt; sm.vand[w] = kand; sm.vor[w] = kor; }
-    __syncthreads();
-    nlt = 0;
-#pragma unroll
-    for (int i = 0; i < kFitWaves; ++i) { nlt += sm.isum[i]; kand &= sm.vand[i]; kor |= sm.vor[i]; }
-  }
+  STAMP(37);
   const uint64_t vary = kand ^ kor;
-  const bool lds_sort = m <= kSortCap;
-  if (!lds_sort)
+  const bool lds_sort = SMALL || m <= kSortCap;
+  if (!lds_sort) {  // the sort runs on the global key copy
+    __syncthreads();
     for (int i = threadIdx.x; i < kSortCap; i += blockDim.x) C.gkeys[i] = lk[i];
+  }
   __syncthreads();
   STAMP(2);
 
   uint32_t *cnt = reinterpret_cast<uint32_t *>(dyn_lds + kOffCnt);
   uint32_t *run = reinterpret_cast<uint32_t *>(dyn_lds + kOffRun);
   if (lds_sort) {
-    const uint16_t *perm = block_sort_perm<uint16_t>(
+    const uint16_t *perm = block_sort_perm<uint16_t, SMALL>(
         lk, reinterpret_cast<uint16_t *>(dyn_lds + kOffPosA),
         reinterpret_cast<uint16_t *>(dyn_lds + kOffPosB), m, vary, cnt, run, sm);
     STAMP(3);
     if (cat) fit_categorical<uint16_t>(A, C, sm, H, slot, lk, perm, m);
+    else if (SMALL) fit_continuous<true, uint16_t, 1>(A, C, sm, H, slot, ob, perm, m, nlt);
     else if (m + 1 <= kMixLds) fit_continuous<true, uint16_t>(A, C, sm, H, slot, ob, perm, m, nlt);
     else fit_continuous<false, uint16_t>(A, C, sm, H, slot, ob, perm, m, nlt);
-  } else {
+  } else if (!SMALL) {
     const uint32_t *perm =
         block_sort_perm<uint32_t>(C.gkeys, C.gpa, C.gpb, m, vary, cnt, run, sm);
     STAMP(3);
@@ -1088,13 +1118,13 @@ __device__ __forceinline__ void fit_slot(const FitArgs &A, unsigned char *dyn_ld
 __global__ __launch_bounds__(kFitThreads) void k_split(FitArgs A, uint8_t *__restrict__ below) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn_lds[];
   __shared__ FitShared sm;
-  if (threadIdx.x == 0) sm.np.n = -1;
   FitCtx C;
   C.lds = dyn_lds;
   C.gkeys = reinterpret_cast<uint64_t *>(A.sortbuf);
   C.gpa = reinterpret_cast<uint32_t *>(A.sortbuf + 8 * A.scap);
   C.gpb = C.gpa + A.scap;
-  const Split t = compute_split(A, C, sm);
+  const double none[4] = {0.0, 0.0, 0.0, 0.0};
+  const Split t = compute_split(A, C, sm, false, none);
   for (int64_t j = threadIdx.x; j < A.n; j += blockDim.x)
     below[j] = is_below(t, sort_key(A.losses[j]), (uint32_t)j) ? 1 : 0;
 }
@@ -1107,13 +1137,11 @@ __global__ __launch_bounds__(256) void k_prep(const tpe_hp *__restrict__ hps,
                                               MixInfo *__restrict__ info, Coef *__restrict__ coef,
                                               int64_t kcap, double *__restrict__ scratch) {
   __shared__ FitShared sm;
-  if (threadIdx.x == 0) sm.np.n = -1;
   const int hp = blockIdx.x, side = blockIdx.y;
   const int64_t slot = 2 * (int64_t)hp + side;
-  const tpe_hp H = hps[hp];
   const int K = info[slot].K;
   __syncthreads();
-  prep_slot(H, slot, K, mw + slot * kcap, mmu + slot * kcap, msig + slot * kcap, info, coef, kcap,
+  prep_slot(hps + hp, slot, K, mw + slot * kcap, mmu + slot * kcap, msig + slot * kcap, info, coef, kcap,
             scratch + slot * kcap, sm);
 }
 
@@ -1127,11 +1155,17 @@ extern "C" int tpe_debug_stamps(unsigned long long *out) {
 namespace tpe {
 #endif
 
-const void *fit_kernel_fn() { return reinterpret_cast<const void *>(&k_fit); }
+bool fit_small(int64_t n) { return n <= kMergeMax; }
+
+const void *fit_kernel_fn(bool small) {
+  return small ? reinterpret_cast<const void *>(&k_fit<true>)
+               : reinterpret_cast<const void *>(&k_fit<false>);
+}
 
 hipError_t launch_fit(const FitArgs &a, int32_t n_hp, hipStream_t st) {
   if (n_hp <= 0) return hipSuccess;
-  k_fit<<<dim3(n_hp, 2), kFitThreads, kFitLds, st>>>(a);
+  if (fit_small(a.n)) k_fit<true><<<dim3(n_hp, 2), kFitThreads, kFitLds, st>>>(a);
+  else k_fit<false><<<dim3(n_hp, 2), kFitThreads, kFitLds, st>>>(a);
   return hipGetLastError();
 }
 

@@ -185,7 +185,8 @@ struct FitArgs {
 // ---- launch wrappers (tpe_fit.hip / tpe_kernels.hip) ----
 hipError_t launch_split(const FitArgs &a, uint8_t *below, hipStream_t st);
 hipError_t launch_fit(const FitArgs &a, int32_t n_hp, hipStream_t st);
-const void *fit_kernel_fn();               // k_fit's host stub (graph node lookup)
+bool fit_small(int64_t n);                 // k_fit<true> (all-LDS variant) serves n trials
+const void *fit_kernel_fn(bool small);     // k_fit's host stub (graph node lookup)
 bool is_draw_kernel_fn(const void *f);     // one of k_draw's / k_draw_sorted's host stubs
 bool is_sorted_draw_kernel_fn(const void *f);
 const void *lattice_draw_kernel_fn();      // k_lattice<true> (lattice + fused draw)

@@ -47,7 +47,8 @@ def main(cfg, slots):
     print('kernel span: %.1f us' % ((st[:2 * P, 10].max() - t0) / 100.0))
     sub = {16: 'sd.zero', 17: 'sd.hist', 18: 'sd.bar1', 19: 'sd.scan', 20: 'sd.bar2',
            21: 'ms.load', 22: 'ms.bitonic64', 23: 'ms.bar', 24: 'ms.L64', 25: 'ms.L128',
-           26: 'ms.L256', 27: 'ms.L512', 28: 'np.plan', 29: 'np.leaves', 30: 'np.end'}
+           26: 'ms.L256', 27: 'ms.L512', 28: 'np.plan', 29: 'np.leaves', 30: 'np.end',
+           31: 'k.zero', 32: 'k.load', 33: 'k.wred', 34: 'k.bar', 35: 'g.load', 36: 'g.scan', 37: 'g.write'}
     for slot in range(min(2 * P, 4)):
         row = st[slot]
         print('slot %d last sub-phase stamps (us from slot start): ' % slot + ' '.join(
