@@ -266,7 +266,7 @@ def main():
     ap.add_argument('--parallelism', default='auto', choices=['auto', 'single', 'sharded'],
                     help="auto: the config's multi-GPU mode when N > 1; 'sharded' forces the "
                          "candidate-sharded path (RCCL all-gather + device merge) even at N = 1")
-    ap.add_argument('--traffic-json', default=os.path.join(ROOT, 'profiles', 'traffic.json'))
+    ap.add_argument('--traffic-json', default=os.path.join(ROOT, 'traffic.json'))
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))

@@ -23,6 +23,7 @@
 using namespace tpe;
 
 static int lse_shift_min();
+static bool wave_tiles_on();
 
 struct tpe_engine {
   int32_t device = 0;
@@ -422,7 +423,8 @@ int32_t set_score_groups(ScoreArgs &a, const int *kinds, int n_slots, int64_t cn
   auto weight = [](int kind) {
     switch (kind) {
       case KIND_ERF_G: case KIND_ERF_L: return 0;
-      case KIND_LSE_G: case KIND_LSE_L: case KIND_LSE_G1: case KIND_LSE_L1: return 1;
+      case KIND_LSE_G: case KIND_LSE_L: case KIND_LSE_G1: case KIND_LSE_L1:
+      case KIND_LSE_GW: case KIND_LSE_LW: return 1;
       case KIND_LAT: return 2;
       default: return 3;
     }
@@ -434,7 +436,7 @@ int32_t set_score_groups(ScoreArgs &a, const int *kinds, int n_slots, int64_t cn
       if (weight(kinds[j]) != pass) { j = k; continue; }
       if (a.n_groups == kMaxGroups) return -1;
       const int g = a.n_groups++;
-      const int64_t tc = 64 * tile_rows(kinds[j]);
+      const int64_t tc = tile_cands(kinds[j]);
       const int32_t nt = (int32_t)((std::max<int64_t>(cn, 0) + tc - 1) / tc);
       a.grp_kind[g] = kinds[j];
       a.grp_slot0[g] = j;
@@ -634,8 +636,19 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
   int64_t c0 = 0;
   do {
     const int64_t cn = std::min(chunk, n_cand - c0);
+    // large draws: each draw block writes its candidates value-bucketed (LSE
+    // and per-candidate erf slots) with their positions; the log-sum-exp
+    // tiles then skip the component blocks that are exact zeros for them,
+    // on wave tiles when the wave-wide exponent is on (prune mode 2)
+    const bool sorted_draw = !fuse_draw && table_draw &&
+                             cn * n_sug * n_level >= ((int64_t)1 << 22);
+    std::vector<int> ck(kinds);
+    if (sorted_draw && p->prune_mode > 1 && wave_tiles_on())
+      for (int &k : ck)
+        k = (k == KIND_LSE_G || k == KIND_LSE_G1) ? KIND_LSE_GW
+          : (k == KIND_LSE_L || k == KIND_LSE_L1) ? KIND_LSE_LW : k;
     ScoreArgs grid{};
-    const int32_t pstride = set_score_groups(grid, kinds.data(), n_level, cn);
+    const int32_t pstride = set_score_groups(grid, ck.data(), n_level, cn);
     if (pstride < 0) return fail(h, TPE_E_INVALID, "level slots not grouped by lpdf kind");
     int rc = ensure_suggest_state(h, p, n_sug, (size_t)n_sug * p->P * pstride);
     if (rc) return rc;
@@ -655,11 +668,6 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
     a.cand_slot0 = 0;
     for (int i = 0; i < kInlineSeeds && i < n_sug; ++i) a.seed_inline[i] = p->h_seeds[i];
     a.n_inline_seeds = (int32_t)std::min<int64_t>(n_sug, kInlineSeeds);
-    // large draws: each draw block writes its candidates value-bucketed (LSE
-    // and per-candidate erf slots) with their positions; the log-sum-exp
-    // tiles then skip the component blocks that are exact zeros for them
-    const bool sorted_draw = !fuse_draw && table_draw &&
-                             cn * n_sug * n_level >= ((int64_t)1 << 22);
     a.lse_pos = sorted_draw ? 1 : 0;
     a.lse_prune = sorted_draw ? p->prune_mode : 0;
     a.lse_shift_min = lse_shift_min();
@@ -1507,6 +1515,16 @@ int tpe_plan_sample_prior(tpe_plan_t p, const uint64_t *seeds, int64_t n_sug, tp
 }
 
 // lse_prune mode 2's smallest mixture (TPE_SHIFT_MIN_K overrides; tuning)
+// log-sum-exp wave tiles on the pruned path (TPE_WAVE_TILES=0: 8-wave
+// component-split tiles everywhere, for A/B measurements)
+static bool wave_tiles_on() {
+  static const bool v = [] {
+    const char *e = std::getenv("TPE_WAVE_TILES");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return v;
+}
+
 static int lse_shift_min() {
   static const int v = [] {
     const char *e = std::getenv("TPE_SHIFT_MIN_K");

@@ -20,8 +20,20 @@ constexpr int kMaxLeaves = 160;  // numpy pairwise leaves per 8192 chunk (<=128)
 // KIND_LSE_G1 / KIND_LSE_L1: the log-sum-exp kinds on one-row (64-candidate)
 // tiles, picked by run_level when two-row tiles would give the CUs too few,
 // unevenly shared blocks
+// KIND_LSE_GW / KIND_LSE_LW: the log-sum-exp kinds on value-bucketed
+// candidates with the block skip and the wave-wide exponent: every wave owns
+// its own 128 candidates and all of both mixtures' live components (no
+// cross-wave partials); a block is 8 such wave tiles
 enum { KIND_LSE_G = 0, KIND_LSE_L = 1, KIND_ERF_G = 2, KIND_ERF_L = 3, KIND_CAT = 4,
-       KIND_LAT = 5, KIND_LSE_G1 = 6, KIND_LSE_L1 = 7 };
+       KIND_LAT = 5, KIND_LSE_G1 = 6, KIND_LSE_L1 = 7, KIND_LSE_GW = 8, KIND_LSE_LW = 9 };
+
+__host__ __device__ constexpr bool kind_lse(int k) {
+  return k == KIND_LSE_G || k == KIND_LSE_L || k == KIND_LSE_G1 || k == KIND_LSE_L1 ||
+         k == KIND_LSE_GW || k == KIND_LSE_LW;
+}
+__host__ __device__ constexpr bool kind_logn(int k) {
+  return k == KIND_LSE_L || k == KIND_LSE_L1 || k == KIND_LSE_LW || k == KIND_ERF_L;
+}
 
 __host__ __device__ inline int score_kind(const tpe_hp &h) {
   if (h.family == TPE_CAT) return KIND_CAT;
@@ -35,6 +47,14 @@ __host__ __device__ constexpr int tile_rows(int kind) {
   return (kind == KIND_ERF_G || kind == KIND_ERF_L || kind == KIND_LSE_G1 || kind == KIND_LSE_L1)
              ? 1
          : (kind == KIND_CAT || kind == KIND_LAT) ? 4 : 2;
+}
+// waves of a block holding their own candidates (wave tiles), else 1
+__host__ __device__ constexpr int tile_waves(int kind) {
+  return (kind == KIND_LSE_GW || kind == KIND_LSE_LW) ? 8 : 1;
+}
+// candidates of one scoring block of the kind
+__host__ __device__ constexpr int tile_cands(int kind) {
+  return 64 * tile_rows(kind) * tile_waves(kind);
 }
 constexpr int kMaxGroups = 8;  // runs of one lpdf kind per launch (a level has <= 7)
 constexpr int kNumCUs = 256;   // MI355X (gfx950): 8 XCDs x 32 CUs

@@ -104,9 +104,8 @@ __global__ __launch_bounds__(kDrawThreads) void k_draw_sorted(ScoreArgs A, int32
   double *out = const_cast<double *>(A.cand) + off;
   const int t = threadIdx.x;
   const int kind = slot_kind(A, slot);
-  const bool bucket = kind == KIND_LSE_G || kind == KIND_LSE_L || kind == KIND_LSE_G1 ||
-                      kind == KIND_LSE_L1 || kind == KIND_ERF_G || kind == KIND_ERF_L;
-  const bool lg = kind == KIND_LSE_L || kind == KIND_LSE_L1 || kind == KIND_ERF_L;
+  const bool bucket = kind_lse(kind) || kind == KIND_ERF_G || kind == KIND_ERF_L;
+  const bool lg = kind_logn(kind);
   double lo = INFINITY, hi = -INFINITY;
 #pragma unroll 1
   for (int i = t; i < n; i += kDrawThreads) {

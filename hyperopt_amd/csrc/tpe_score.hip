@@ -171,7 +171,7 @@ __device__ __forceinline__ float envelope_bound(const float4 e, const LseWindow 
 // their envelopes, tpe_internal.hpp kLseDeadBase), a ballot gives the round's
 // live blocks, and only those are evaluated, in the same order as the full
 // loop.  prune = false: every block is live.
-template <int KR, bool CENSUS>
+template <int KR, bool CENSUS, int STRIDE = kWaves>
 __device__ __forceinline__ void lse_chunks(KDbl *__restrict__ cs, const Coef *__restrict__ cv,
                                            int c0, int nb, const double (&y)[KR],
                                            LseAcc (&out)[KR], bool prune, LseWindow win,
@@ -181,8 +181,8 @@ __device__ __forceinline__ void lse_chunks(KDbl *__restrict__ cs, const Coef *__
 #pragma unroll
   for (int r = 0; r < KR; ++r) { m[r] = -INFINITY; s[r] = 0.0; }
   const int nch = (nb + kChunk - 1) / kChunk;
-  for (int r0 = c0; r0 < nch; r0 += kWaves * 64) {
-    const int c = r0 + kWaves * lane;
+  for (int r0 = c0; r0 < nch; r0 += STRIDE * 64) {
+    const int c = r0 + STRIDE * lane;
     const int k0 = c * kChunk;
     const bool has0 = c < nch, has1 = has0 && k0 + kGroup < nb;
     bool live0 = has0, live1 = has1;
@@ -216,7 +216,7 @@ __device__ __forceinline__ void lse_chunks(KDbl *__restrict__ cs, const Coef *__
       const int j = g ? j1 : j0;
       if (g) m1 &= m1 - 1;
       else m0 &= m0 - 1;
-      const int kg = (r0 + kWaves * j) * kChunk + g * kGroup;
+      const int kg = (r0 + STRIDE * j) * kChunk + g * kGroup;
       CoefGroup cgp;
       load_group(cs, kg, cgp);
       lse_group<KR, false>(cgp, kg, nb, y, m, s);
@@ -266,7 +266,7 @@ __device__ __forceinline__ void lse_group_shifted(const CoefGroup &g, double M,
   for (int r = 0; r < KR; ++r) s[r] += (double)f[r];
 }
 
-template <int KR, bool CENSUS>
+template <int KR, bool CENSUS, int STRIDE = kWaves>
 __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
                                                    const Coef *__restrict__ cv, int c0, int nb,
                                                    const double (&y)[KR], const bool (&valid)[KR],
@@ -277,8 +277,8 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
   const double *tb = reinterpret_cast<const double *>(cv);
   // pass 1: the largest live block bound of the wave's chunks
   float bmax = -INFINITY;
-  for (int r0 = c0; r0 < nch; r0 += kWaves * 64) {
-    const int c = r0 + kWaves * lane;
+  for (int r0 = c0; r0 < nch; r0 += STRIDE * 64) {
+    const int c = r0 + STRIDE * lane;
     const int k0 = c * kChunk;
     if (c < nch) {
       const float b0 = envelope_bound(*reinterpret_cast<const float4 *>(tb + coef_off(k0, 3)), win);
@@ -302,8 +302,8 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
   for (int attempt = 0;; ++attempt) {
 #pragma unroll
     for (int r = 0; r < KR; ++r) s[r] = 0.0;
-    for (int r0 = c0; r0 < nch; r0 += kWaves * 64) {
-      const int c = r0 + kWaves * lane;
+    for (int r0 = c0; r0 < nch; r0 += STRIDE * 64) {
+      const int c = r0 + STRIDE * lane;
       const int k0 = c * kChunk;
       const bool has0 = c < nch, has1 = has0 && k0 + kGroup < nb;
       bool live0 = false, live1 = false;
@@ -334,7 +334,7 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
         if (g) m1 &= m1 - 1;
         else m0 &= m0 - 1;
         CoefGroup cgp;
-        load_group(cs, (r0 + kWaves * j) * kChunk + g * kGroup, cgp);
+        load_group(cs, (r0 + STRIDE * j) * kChunk + g * kGroup, cgp);
         lse_group_shifted<KR>(cgp, M, y, s);
       }
     }
@@ -544,17 +544,19 @@ __device__ unsigned long long g_score_stamps[8192][4];
 struct ScoreSmem {
   double2 wpart[2][kWaves][kRMax][64];  // per-wave partials (below, above)
   double2 merged[2][kRMax][64];         // merged per (mixture, candidate row)
+  double best_s[kWaves], best_v[kWaves];  // wave tiles: each wave's argmax
+  int64_t best_i[kWaves];
 };
 
 template <int KIND, bool CENSUS>
 __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, int slot, int tile,
                                            int ntiles) {
   constexpr int KR = tile_rows(KIND);
-  constexpr bool LSE = KIND == KIND_LSE_G || KIND == KIND_LSE_L || KIND == KIND_LSE_G1 ||
-                       KIND == KIND_LSE_L1;
+  constexpr bool LSE = kind_lse(KIND);
+  constexpr bool WT = tile_waves(KIND) > 1;  // wave tiles: own candidates, all components
   constexpr bool ERF = KIND == KIND_ERF_G || KIND == KIND_ERF_L;
   constexpr bool LAT = KIND == KIND_LAT;  // quantized, looked up on its value lattice
-  constexpr bool LOGN = KIND == KIND_LSE_L || KIND == KIND_LSE_L1 || KIND == KIND_ERF_L;
+  constexpr bool LOGN = kind_logn(KIND);
   const int s = blockIdx.y;
   const int hp = A.level_hps[slot];
   const tpe_hp H = A.hps[hp];
@@ -583,7 +585,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
   double x[KR], y[KR], ub[KR], lb[KR];
 #pragma unroll
   for (int r = 0; r < KR; ++r) {
-    li[r] = (int64_t)tile * (64 * KR) + r * 64 + lane;
+    li[r] = (int64_t)tile * tile_cands(KIND) + (WT ? wave * 64 * KR : 0) + r * 64 + lane;
     valid[r] = li[r] < A.n_cand;
     x[r] = valid[r] ? cand[li[r]] : (LOGN ? 1.0 : 0.0);
     y[r] = ub[r] = lb[r] = 0.0;
@@ -595,6 +597,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
     }
   }
 
+  LseAcc wt_acc[2][KR];  // wave tiles: the wave's final sums
   if constexpr (LSE || ERF) {
     // warm this XCD's L2 with both mixtures' coefficient lines: one dword per
     // 128-B line, issued before the component loop, so the loop's scalar loads
@@ -654,13 +657,36 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
         // (lse_chunks_shifted's guard), else the exact per-group-lift loop
         // (mixtures of >= lse_shift_min components: fewer leave too few
         // terms near a wave-wide exponent for most waves to pass its guard)
+        // (wave tiles: the shifted form over every chunk in one pass -- within
+        // 3e-7 of the exact sum, large mixtures only, as for 8-wave tiles;
+        // smaller ones keep the exact per-group lift below)
+        constexpr int ST = WT ? 1 : kWaves;
+        const int cw0 = WT ? 0 : wv;
         const bool shifted = prune && A.lse_prune > 1 && K >= A.lse_shift_min &&
                              win.thr > -INFINITY &&
-                             lse_chunks_shifted<KR, CENSUS>(uniform_ptr(cm), cm, wv, K, y, valid,
-                                                            lacc[mix], win, nvalid, lcen);
-        if (!shifted)
-          lse_chunks<KR, CENSUS>(uniform_ptr(cm), cm, wv, K, y, lacc[mix], prune, win, nvalid,
-                                 lcen);
+                             lse_chunks_shifted<KR, CENSUS, ST>(uniform_ptr(cm), cm, cw0, K, y,
+                                                                valid, lacc[mix], win, nvalid,
+                                                                lcen);
+        if (!shifted) {
+          if constexpr (WT) {
+            // the exact loop in the 8-wave tile's association: chunk owner
+            // v = c (mod kWaves) as 8 passes, merged in owner order -- the
+            // same sums, bit for bit, as the component-split tile's waves
+            for (int v = 0; v < kWaves; ++v) {
+              LseAcc part[KR];
+              lse_chunks<KR, CENSUS, kWaves>(uniform_ptr(cm), cm, v, K, y, part, prune, win,
+                                             nvalid, lcen);
+#pragma unroll
+              for (int r = 0; r < KR; ++r) {
+                if (v == 0) lacc[mix][r] = part[r];
+                else lse_merge(lacc[mix][r], part[r]);
+              }
+            }
+          } else {
+            lse_chunks<KR, CENSUS, kWaves>(uniform_ptr(cm), cm, wv, K, y, lacc[mix], prune, win,
+                                           nvalid, lcen);
+          }
+        }
       } else {
         erf_chunks<KR, LOGN, CENSUS>(uniform_ptr(cm), wv, K, ub, lb, valid, wlo, whi, exact, pacc[mix], cen);
       }
@@ -688,6 +714,13 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
         atomicAdd(A.census + 5, c2[1]);
       }
     }
+    if constexpr (WT) {
+      // the wave's sums are final: kept in registers for the finalize
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int r = 0; r < KR; ++r) wt_acc[q][r] = lacc[q][r];
+    } else {
 #pragma unroll
     for (int q = 0; q < 2; ++q)
 #pragma unroll
@@ -712,9 +745,10 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
       sm.merged[q][r][lane] = v0;
     }
     __syncthreads();
+    }
   }
   SSTAMP(1);
-  if (wave != 0) return;
+  if (!WT && wave != 0) return;
 
   // ---- finalize the tile (wave 0): lpdfs, EI, argmax (numpy semantics)
   double best_s = NAN, best_v = NAN;
@@ -725,7 +759,8 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
     double lpb, lpa;
     if constexpr (LSE) {
       const double LN2 = 0.6931471805599453;
-      const double2 b = sm.merged[0][r][lane], a = sm.merged[1][r][lane];
+      const double2 b = WT ? make_double2(wt_acc[0][r].m, wt_acc[0][r].s) : sm.merged[0][r][lane];
+      const double2 a = WT ? make_double2(wt_acc[1][r].m, wt_acc[1][r].s) : sm.merged[1][r][lane];
       lpb = (b.x == -INFINITY) ? NAN : (b.x + log2(b.y)) * LN2;
       lpa = (a.x == -INFINITY) ? NAN : (a.x + log2(a.y)) * LN2;
       if constexpr (LOGN) { const double lx = log(x[r]); lpb -= lx; lpa -= lx; }
@@ -754,6 +789,14 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
     if (better(sc, gi, best_s, best_i)) { best_s = sc; best_v = x[r]; best_i = gi; }
   }
   wave_best(best_s, best_v, best_i);
+  if constexpr (WT) {  // the block's argmax over its wave tiles (better() orders ties)
+    if (lane == 0) { sm.best_s[wave] = best_s; sm.best_v[wave] = best_v; sm.best_i[wave] = best_i; }
+    __syncthreads();
+    if (wave != 0) return;
+    const int w = lane < kWaves ? lane : 0;
+    best_s = sm.best_s[w]; best_v = sm.best_v[w]; best_i = lane < kWaves ? sm.best_i[w] : -1;
+    wave_best(best_s, best_v, best_i);
+  }
   Partial *pbase = A.partial + ((int64_t)s * A.n_hp + hp) * A.pstride;
   int is_last = 0;
   if (lane == 0) {
@@ -820,6 +863,8 @@ void k_score(ScoreArgs A) {
     case KIND_LSE_L: score_tile<KIND_LSE_L, CENSUS>(A, sm, slot, tile, nt); break;
     case KIND_LSE_G1: score_tile<KIND_LSE_G1, CENSUS>(A, sm, slot, tile, nt); break;
     case KIND_LSE_L1: score_tile<KIND_LSE_L1, CENSUS>(A, sm, slot, tile, nt); break;
+    case KIND_LSE_GW: score_tile<KIND_LSE_GW, CENSUS>(A, sm, slot, tile, nt); break;
+    case KIND_LSE_LW: score_tile<KIND_LSE_LW, CENSUS>(A, sm, slot, tile, nt); break;
     case KIND_ERF_G: if constexpr (ERFK) score_tile<KIND_ERF_G, CENSUS>(A, sm, slot, tile, nt); break;
     case KIND_ERF_L: if constexpr (ERFK) score_tile<KIND_ERF_L, CENSUS>(A, sm, slot, tile, nt); break;
     case KIND_LAT: score_tile<KIND_LAT, CENSUS>(A, sm, slot, tile, nt); break;
