@@ -439,10 +439,11 @@ __global__ __launch_bounds__(256) void k_micro(int iters, double *sink) {
   } else if constexpr (WHICH == 5) {
     // one log-sum-exp pair as the one-exponent-per-wave loop computes it
     // (lse_group_shifted): alpha - M once per component per lane, then two
-    // FMAs, cvt, exp2, fp32 tree, fp64 sum; 4 candidates x 8 components
-    double y[4], sm[4];
+    // FMAs (y' and y'^2 per candidate), cvt, exp2, fp32 tree, fp64 sum; 4
+    // candidates x 8 components
+    double y[4], y2[4], sm[4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) { y[c] = 1e-3 * (t + c); sm[c] = 0.0; }
+    for (int c = 0; c < 4; ++c) { y[c] = 1e-3 * (t + c); y2[c] = y[c] * y[c]; sm[c] = 0.0; }
     double cx[8], cy[8], cz[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) { cx[k] = -0.1 * k; cy[k] = 0.01 * k; cz[k] = -0.5 - 0.01 * k; }
@@ -456,7 +457,7 @@ __global__ __launch_bounds__(256) void k_micro(int iters, double *sink) {
         float e[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k)
-          e[k] = __builtin_amdgcn_exp2f((float)fma(fma(cz[k], y[c], cy[k]), y[c], am[k]));
+          e[k] = __builtin_amdgcn_exp2f((float)fma(cz[k], y2[c], fma(cy[k], y[c], am[k])));
 #pragma unroll
         for (int w = 4; w > 0; w >>= 1)
 #pragma unroll

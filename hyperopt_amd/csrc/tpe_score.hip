@@ -240,9 +240,13 @@ __device__ __forceinline__ void lse_chunks(KDbl *__restrict__ cs, const Coef *__
 // valid lane's sum must be >= 2^-4 (its dominant terms within ~4 of M, error
 // <= 3e-7); otherwise (a spread-out tile) the wave returns false and the
 // exact per-group-lift loop runs instead.
+// t - M = (alpha - M) + beta y' + gamma y'^2 as fma(gamma, y'^2, fma(beta, y',
+// alpha - M)): each FMA reads one scalar (SGPR) coefficient, so no VALU move
+// of a second one is needed (one scalar operand per VALU instruction).
 template <int KR>
 __device__ __forceinline__ void lse_group_shifted(const CoefGroup &g, double M,
-                                                  const double (&y)[KR], double (&s)[KR]) {
+                                                  const double (&y)[KR], const double (&y2)[KR],
+                                                  double (&s)[KR]) {
   // two halves of 4 components: the shifted alphas and the fp32 terms of a
   // half stay in few VGPRs; a lane's group sum is (h0 tree) + (h1 tree)
   float f[KR];
@@ -257,7 +261,7 @@ __device__ __forceinline__ void lse_group_shifted(const CoefGroup &g, double M,
 #pragma unroll
       for (int j = 0; j < kGroup / 2; ++j)
         e[j] = __builtin_amdgcn_exp2f(
-            (float)fma(fma(g.z[4 * h + j], y[r], g.y[4 * h + j]), y[r], am[j]));
+            (float)fma(g.z[4 * h + j], y2[r], fma(g.y[4 * h + j], y[r], am[j])));
       const float t = (e[0] + e[2]) + (e[1] + e[3]);
       f[r] = h ? f[r] + t : t;
     }
@@ -298,7 +302,9 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
   // then in (1/4, 1/2]) and the wave runs once more; failing that (or a sum
   // that underflowed), the exact loop
   double M = __builtin_amdgcn_readfirstlane((int)ceil((double)bmax)) + 1.0;
-  double s[KR];
+  double s[KR], y2[KR];
+#pragma unroll
+  for (int r = 0; r < KR; ++r) y2[r] = y[r] * y[r];
   for (int attempt = 0;; ++attempt) {
 #pragma unroll
     for (int r = 0; r < KR; ++r) s[r] = 0.0;
@@ -335,7 +341,7 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
         else m0 &= m0 - 1;
         CoefGroup cgp;
         load_group(cs, (r0 + STRIDE * j) * kChunk + g * kGroup, cgp);
-        lse_group_shifted<KR>(cgp, M, y, s);
+        lse_group_shifted<KR>(cgp, M, y, y2, s);
       }
     }
     bool ok = true;
