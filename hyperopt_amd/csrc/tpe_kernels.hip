@@ -412,9 +412,9 @@ __global__ __launch_bounds__(256) void k_micro(int iters, double *sink) {
     // one log-sum-exp (candidate, component) pair exactly as k_score computes
     // it (two FMAs, max pass, exp2 of the fp64 difference, fp64 sum): 4
     // candidates per lane x 8 register-resident components per iteration
-    double y[4], m[4], sm[4];
+    double y[4], y2[4], m[4], sm[4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) { y[c] = 1e-3 * (t + c); sm[c] = 0.0; }
+    for (int c = 0; c < 4; ++c) { y[c] = 1e-3 * (t + c); y2[c] = y[c] * y[c]; sm[c] = 0.0; }
     double cx[8], cy[8], cz[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) { cx[k] = -0.1 * k; cy[k] = 0.01 * k; cz[k] = -0.5 - 0.01 * k; }
@@ -423,10 +423,10 @@ __global__ __launch_bounds__(256) void k_micro(int iters, double *sink) {
       for (int c = 0; c < 4; ++c) {
         m[c] = -INFINITY;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) m[c] = fmax(m[c], fma(fma(cz[k], y[c], cy[k]), y[c], cx[k]));
+        for (int k = 0; k < 8; ++k) m[c] = fmax(m[c], fma(cz[k], y2[c], fma(cy[k], y[c], cx[k])));
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const double tt = fma(fma(cz[k], y[c], cy[k]), y[c], cx[k]);
+          const double tt = fma(cz[k], y2[c], fma(cy[k], y[c], cx[k]));
           sm[c] += (double)__builtin_amdgcn_exp2f((float)(tt - m[c]));
         }
         y[c] += 1e-9;

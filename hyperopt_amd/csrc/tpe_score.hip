@@ -109,14 +109,15 @@ __device__ __forceinline__ void load_group(KDbl *__restrict__ cs, int k, CoefGro
 // m = -inf and scores NaN as well.
 template <int KR, bool TAIL>
 __device__ __forceinline__ void lse_group(const CoefGroup &g, int k, int nb,
-                                          const double (&y)[KR], double (&m)[KR],
-                                          double (&s)[KR]) {
+                                          const double (&y)[KR], const double (&y2)[KR],
+                                          double (&m)[KR], double (&s)[KR]) {
 #pragma unroll
   for (int r = 0; r < KR; ++r) {
     double t[kGroup];
 #pragma unroll
     for (int j = 0; j < kGroup; ++j) {
-      t[j] = fma(fma(g.z[j], y[r], g.y[j]), y[r], g.x[j]);
+      // alpha + beta y' + gamma y'^2, one scalar coefficient per FMA
+      t[j] = fma(g.z[j], y2[r], fma(g.y[j], y[r], g.x[j]));
       if (TAIL && k + j >= nb) t[j] = -INFINITY;  // wave-uniform
     }
     // group max as a tree (fmax drops NaN terms)
@@ -177,9 +178,9 @@ __device__ __forceinline__ void lse_chunks(KDbl *__restrict__ cs, const Coef *__
                                            LseAcc (&out)[KR], bool prune, LseWindow win,
                                            int nvalid, LseCensus &cen) {
   const int lane = threadIdx.x & 63;
-  double m[KR], s[KR];
+  double m[KR], s[KR], y2[KR];
 #pragma unroll
-  for (int r = 0; r < KR; ++r) { m[r] = -INFINITY; s[r] = 0.0; }
+  for (int r = 0; r < KR; ++r) { m[r] = -INFINITY; s[r] = 0.0; y2[r] = y[r] * y[r]; }
   const int nch = (nb + kChunk - 1) / kChunk;
   for (int r0 = c0; r0 < nch; r0 += STRIDE * 64) {
     const int c = r0 + STRIDE * lane;
@@ -219,7 +220,7 @@ __device__ __forceinline__ void lse_chunks(KDbl *__restrict__ cs, const Coef *__
       const int kg = (r0 + STRIDE * j) * kChunk + g * kGroup;
       CoefGroup cgp;
       load_group(cs, kg, cgp);
-      lse_group<KR, false>(cgp, kg, nb, y, m, s);
+      lse_group<KR, false>(cgp, kg, nb, y, y2, m, s);
     }
   }
 #pragma unroll
