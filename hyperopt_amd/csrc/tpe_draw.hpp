@@ -59,6 +59,17 @@ __device__ __forceinline__ int pick_cdf(const double *cdf, int K, double u) {
   return lo;
 }
 
+// the rejection sampler's Philox pair and Box-Muller normal, out of line: its
+// register footprint is what every kernel that can reach the fallback
+// allocates, common path or not
+__device__ __attribute__((noinline)) inline Draw draw4_ool(uint64_t seed, uint64_t gi,
+                                                           uint32_t stream, uint32_t it) {
+  return draw4(seed, gi, stream, it);
+}
+__device__ __attribute__((noinline)) inline double box_muller_ool(double u1, double u2) {
+  return sqrt(-2.0 * log(1.0 - u1)) * cospi(2.0 * u2);
+}
+
 // One GMM1/LGMM1/categorical draw (tpe.py:62-93, 216-250; stochastic.py:104);
 // cdf (optional): the weights' inclusive prefix sums.  The rejection sampler
 // is the fallback for mixtures beyond the LDS table.
@@ -78,9 +89,9 @@ __device__ inline double draw_one(const tpe_hp &H, const MixInfo &I,
   Draw d{};
 #pragma unroll 1
   for (uint32_t it = 0; it < 64 && !ok; ++it) {
-    d = draw4(seed, gi, stream, it);
+    d = draw4_ool(seed, gi, stream, it);
     k = cdf ? pick_cdf(cdf, I.K, d.u0) : pick(w, I.K, d.u0 * I.wsum);
-    const double z = sqrt(-2.0 * log(1.0 - d.u1)) * cospi(2.0 * d.u2);
+    const double z = box_muller_ool(d.u1, d.u2);
     const double v = mu[k] + sg[k] * z;
     if (!bounded || (H.low <= v && v < H.high)) { x = v; ok = true; }
   }

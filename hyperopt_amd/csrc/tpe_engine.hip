@@ -24,6 +24,8 @@ using namespace tpe;
 
 static int lse_shift_min();
 static bool wave_tiles_on();
+static bool small_sort_on();
+constexpr int64_t kSmallSortMin = 2048;  // candidates per chunk worth bucketing a small draw
 
 struct tpe_engine {
   int32_t device = 0;
@@ -642,11 +644,24 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
     // on wave tiles when the wave-wide exponent is on (prune mode 2)
     const bool sorted_draw = !fuse_draw && table_draw &&
                              cn * n_sug * n_level >= ((int64_t)1 << 22);
+    // small draws of >= kSmallSortMin candidates: the log-sum-exp slots are
+    // value-bucketed too (k_bucket, stable, <= 8192 per bucketing chunk) and
+    // pruned on the 8-wave tiles
+    bool small_sort = false;
+    if (!sorted_draw && small_sort_on() && cn >= kSmallSortMin)
+      for (int k : kinds) small_sort |= k == KIND_LSE_G || k == KIND_LSE_L || k == KIND_LSE_G1 ||
+                                        k == KIND_LSE_L1;
     std::vector<int> ck(kinds);
     if (sorted_draw && p->prune_mode > 1 && wave_tiles_on())
       for (int &k : ck)
         k = (k == KIND_LSE_G || k == KIND_LSE_G1) ? KIND_LSE_GW
           : (k == KIND_LSE_L || k == KIND_LSE_L1) ? KIND_LSE_LW : k;
+    else if (small_sort)
+      // one-row tiles whatever the batch size: the pruned sums depend on the
+      // tile's candidate window, so a batched suggestion stays bit-identical
+      // to the same seed's single one
+      for (int &k : ck)
+        k = k == KIND_LSE_G ? KIND_LSE_G1 : k == KIND_LSE_L ? KIND_LSE_L1 : k;
     ScoreArgs grid{};
     const int32_t pstride = set_score_groups(grid, ck.data(), n_level, cn);
     if (pstride < 0) return fail(h, TPE_E_INVALID, "level slots not grouped by lpdf kind");
@@ -668,8 +683,8 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
     a.cand_slot0 = 0;
     for (int i = 0; i < kInlineSeeds && i < n_sug; ++i) a.seed_inline[i] = p->h_seeds[i];
     a.n_inline_seeds = (int32_t)std::min<int64_t>(n_sug, kInlineSeeds);
-    a.lse_pos = sorted_draw ? 1 : 0;
-    a.lse_prune = sorted_draw ? p->prune_mode : 0;
+    a.lse_pos = (sorted_draw || small_sort) ? 1 : 0;
+    a.lse_prune = (sorted_draw || small_sort) ? p->prune_mode : 0;
     a.lse_shift_min = lse_shift_min();
     if (fuse_draw) {
       tpe_plan::Prof *pr = nullptr;
@@ -687,8 +702,8 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
     } else {
       CKH(launch_draw(a, table_draw, st));
     }
-    if (erf_level && !sorted_draw) CKH(launch_bucket(a, n_lat, p->d_cpos, st));
-    a.cand_pos = (erf_level || sorted_draw) ? p->d_cpos : nullptr;
+    if ((erf_level || small_sort) && !sorted_draw) CKH(launch_bucket(a, n_lat, p->d_cpos, st));
+    a.cand_pos = (erf_level || sorted_draw || small_sort) ? p->d_cpos : nullptr;
     if (!joined) {
       CKH(hipStreamWaitEvent(st, p->ev_join[0], 0));
       joined = true;
@@ -1521,6 +1536,18 @@ static bool wave_tiles_on() {
   static const bool v = [] {
     const char *e = std::getenv("TPE_WAVE_TILES");
     return !(e && std::atoi(e) == 0);
+  }();
+  return v;
+}
+
+// value-bucketed, pruned log-sum-exp slots on small draws: opt-in
+// (TPE_SMALL_SORT=1).  Measured at config 2 (4096 candidates): the skip drops
+// 80 % of the pairs and k_score from 33 to 23 us, but the extra k_bucket
+// launch costs more than that (suggest 70 -> 78 us)
+static bool small_sort_on() {
+  static const bool v = [] {
+    const char *e = std::getenv("TPE_SMALL_SORT");
+    return e && std::atoi(e) != 0;
   }();
   return v;
 }

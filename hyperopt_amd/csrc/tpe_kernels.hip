@@ -19,6 +19,79 @@ namespace tpe {
 
 constexpr int kSortMax = 8192;  // candidates per bucketing chunk
 
+// Stable counting scatter by an 8-bit bucket: element i of [0, n) goes to
+// position dest(i) = (elements of lower buckets) + (elements of its bucket
+// with a lower index), independent of thread timing (an atomic-increment
+// scatter orders a bucket's elements by arrival, so which scoring tile a
+// candidate lands in -- and the log-sum-exp block skip of that tile --
+// would vary from run to run).  Wave w takes elements [w * per, ...) in
+// order; per (wave, bucket) counts from 8-ballot lane matching, one scan
+// over (bucket, wave), then the same walk writes the destinations.
+// cnt: NW * 256 ints of LDS; every thread of the block calls it.
+__device__ __forceinline__ uint64_t lanes_equal8(uint32_t d, bool v) {
+  uint64_t m = __ballot(v);
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    const bool x = (d >> b) & 1u;
+    const uint64_t bb = __ballot(x);
+    m &= x ? bb : ~bb;
+  }
+  return m;
+}
+
+template <int NW, typename Dest>
+__device__ __forceinline__ void stable_bucket_scatter(const unsigned char *bk, int n, int *cnt,
+                                                      Dest dest) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int per = ((n + NW * 64 - 1) / (NW * 64)) * 64;
+  const int r0 = w * per, r1 = min(n, r0 + per);
+  int *mine = cnt + w * 256;
+  for (int b = lane; b < 256; b += 64) mine[b] = 0;
+  // (a wave's LDS ops complete in order: no barrier between its own rows)
+  for (int base = r0; base < r1; base += 64) {
+    const int i = base + lane;
+    const bool v = i < r1;
+    const uint32_t d = v ? bk[i] : 0u;
+    const uint64_t mt = lanes_equal8(d, v);
+    if (v && lane == __ffsll((long long)mt) - 1) mine[d] += __popcll(mt);
+  }
+  __syncthreads();
+  // bucket b (thread b of the first 256): its total over the waves, a block
+  // scan of the totals, then the (bucket, wave) bases in place
+  static_assert(NW * 64 >= 256, "one thread per bucket");
+  __shared__ int wtot[4];
+  int tot = 0;
+  if (threadIdx.x < 256)
+    for (int q = 0; q < NW; ++q) tot += cnt[q * 256 + threadIdx.x];
+  int x = tot;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63 && w < 4) wtot[w] = x;
+  __syncthreads();
+  if (threadIdx.x < 256) {
+    int acc = x - tot;
+    for (int q = 0; q < w; ++q) acc += wtot[q];
+    for (int q = 0; q < NW; ++q) {
+      const int c = cnt[q * 256 + threadIdx.x];
+      cnt[q * 256 + threadIdx.x] = acc;
+      acc += c;
+    }
+  }
+  __syncthreads();
+  for (int base = r0; base < r1; base += 64) {
+    const int i = base + lane;
+    const bool v = i < r1;
+    const uint32_t d = v ? bk[i] : 0u;
+    const uint64_t mt = lanes_equal8(d, v);
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    if (v) dest(i, mine[d] + __popcll(mt & lt));
+    if (v && lane == __ffsll((long long)mt) - 1) mine[d] += __popcll(mt);
+  }
+}
+
 
 // Candidate draws of one level (all its hps): grid = (blocks, hps of the
 // level, suggestions), one candidate per thread per step.  Counter = (global
@@ -81,7 +154,7 @@ struct SortedDrawLds {
   DrawTableT<CAP> T;
   double xs[kSortedBlock];          // the block's draws, in draw order
   unsigned char bk[kSortedBlock];   // their buckets
-  int32_t hist[kSortBuckets];
+  int32_t cnt[kDrawThreads / 64 * kSortBuckets];  // stable scatter counts / bases
   double red[2][kDrawThreads / 64];
 };
 
@@ -129,44 +202,24 @@ __global__ __launch_bounds__(kDrawThreads) void k_draw_sorted(ScoreArgs A, int32
   }
   const int lane = t & 63, wv = t >> 6;
   if (lane == 0) { L.red[0][wv] = lo; L.red[1][wv] = hi; }
-  for (int b = t; b < kSortBuckets; b += kDrawThreads) L.hist[b] = 0;
   __syncthreads();
   lo = INFINITY; hi = -INFINITY;
 #pragma unroll
   for (int w = 0; w < kDrawThreads / 64; ++w) { lo = fmin(lo, L.red[0][w]); hi = fmax(hi, L.red[1][w]); }
   const double scale = hi > lo ? (double)kSortBuckets / (hi - lo) : 0.0;
   for (int i = t; i < n; i += kDrawThreads) {
-    const double x = L.xs[i];
-    const double key = lg ? log(x) : x;
+    const double key = lg ? log(L.xs[i]) : L.xs[i];
     int b = kSortBuckets - 1;
     if (fabs(key) < INFINITY) b = min(kSortBuckets - 1, max(0, (int)((key - lo) * scale)));
     L.bk[i] = (unsigned char)b;
-    atomicAdd(&L.hist[b], 1);
   }
   __syncthreads();
-  if (t < 64) {  // exclusive scan of the bucket counts, 4 per lane
-    static_assert(kSortBuckets == 256, "4 buckets per lane");
-    int c[4], tot = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) { c[j] = L.hist[4 * lane + j]; tot += c[j]; }
-    int v = tot;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int nb = __shfl_up(v, o, 64);
-      if (lane >= o) v += nb;
-    }
-    int acc = v - tot;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) { L.hist[4 * lane + j] = acc; acc += c[j]; }
-  }
-  __syncthreads();
-  // scatter into the block's slice (32 KB + 16 KB, merged in L2)
+  // scatter into the block's slice (32 KB + 16 KB, merged in L2), stable
   int32_t *po = pos_out + off;
-  for (int i = t; i < n; i += kDrawThreads) {
-    const int p = atomicAdd(&L.hist[L.bk[i]], 1);
+  stable_bucket_scatter<kDrawThreads / 64>(L.bk, n, L.cnt, [&](int i, int p) {
     out[p] = L.xs[i];
     po[p] = (int32_t)(base + i);
-  }
+  });
 }
 
 // Bucket each 8192-candidate chunk of the erf-kind hps by value (counting
@@ -180,13 +233,15 @@ constexpr int kBuckets = 256;
 __global__ __launch_bounds__(1024) void k_bucket(ScoreArgs A, int32_t slot_begin,
                                                  int32_t *__restrict__ pos_out) {
   extern __shared__ __attribute__((aligned(16))) double dyn_lds[];
-  __shared__ int hist[kBuckets];
+  __shared__ int cnt[16 * kBuckets];
   __shared__ double red_lo[16], red_hi[16];
   const int slot = slot_begin + (int)blockIdx.y, s = blockIdx.z;
   const int hp = A.level_hps[slot];
   const tpe_hp H = A.hps[hp];
   const int kind = score_kind(H);
-  if (kind != KIND_ERF_G && kind != KIND_ERF_L) return;
+  // erf kinds always; log-sum-exp kinds when the launch prunes them (lse_pos)
+  const bool lse = kind == KIND_LSE_G || kind == KIND_LSE_L;
+  if (!(kind == KIND_ERF_G || kind == KIND_ERF_L || (lse && A.lse_pos))) return;
   if (!hp_active(H, A.results + (int64_t)s * A.n_hp, A.cond_parent, A.cond_branch)) return;
   const int64_t base = (int64_t)blockIdx.x * kSortMax;
   if (base >= A.n_cand) return;
@@ -195,7 +250,7 @@ __global__ __launch_bounds__(1024) void k_bucket(ScoreArgs A, int32_t slot_begin
   double *cand = const_cast<double *>(A.cand) + off;
   double *xs = dyn_lds;                                        // [8192] values
   unsigned char *bk = reinterpret_cast<unsigned char *>(dyn_lds + kSortMax);  // [8192]
-  const bool lg = kind == KIND_ERF_L;
+  const bool lg = kind == KIND_ERF_L || kind == KIND_LSE_L;
   double lo = INFINITY, hi = -INFINITY;
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
     const double x = cand[i];
@@ -203,7 +258,6 @@ __global__ __launch_bounds__(1024) void k_bucket(ScoreArgs A, int32_t slot_begin
     const double t = lg ? log(fmax(x, 1e-300)) : x;
     if (t == t && fabs(t) < INFINITY) { lo = fmin(lo, t); hi = fmax(hi, t); }
   }
-  for (int b = threadIdx.x; b < kBuckets; b += blockDim.x) hist[b] = 0;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     lo = fmin(lo, __shfl_xor(lo, o, 64));
@@ -221,31 +275,13 @@ __global__ __launch_bounds__(1024) void k_bucket(ScoreArgs A, int32_t slot_begin
     int b = kBuckets - 1;
     if (t == t && fabs(t) < INFINITY) b = min(kBuckets - 1, max(0, (int)((t - lo) * scale)));
     bk[i] = (unsigned char)b;
-    atomicAdd(&hist[b], 1);
-  }
-  __syncthreads();
-  if (threadIdx.x < 64) {  // exclusive scan of the 256 counts: 4 per lane + wave scan
-    static_assert(kBuckets == 256, "4 buckets per lane");
-    int c[4], tot = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) { c[j] = hist[4 * lane + j]; tot += c[j]; }
-    int v = tot;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int n = __shfl_up(v, o, 64);
-      if (lane >= o) v += n;
-    }
-    int acc = v - tot;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) { hist[4 * lane + j] = acc; acc += c[j]; }
   }
   __syncthreads();
   int32_t *po = pos_out + off;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    const int p = atomicAdd(&hist[bk[i]], 1);
+  stable_bucket_scatter<16>(bk, n, cnt, [&](int i, int p) {
     cand[p] = xs[i];
     po[p] = (int32_t)(base + i);
-  }
+  });
 }
 
 // cross-device merge of gathered [world][S][P] results
