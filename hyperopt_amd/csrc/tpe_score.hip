@@ -604,7 +604,6 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
     }
   }
 
-  LseAcc wt_acc[2][KR];  // wave tiles: the wave's final sums
   if constexpr (LSE || ERF) {
     // warm this XCD's L2 with both mixtures' coefficient lines: one dword per
     // 128-B line, issued before the component loop, so the loop's scalar loads
@@ -694,6 +693,13 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
                                            nvalid, lcen);
           }
         }
+        if constexpr (WT) {
+          // the wave's final sums of this mixture wait in its own LDS rows
+          // (registers stay free for the next mixture's loop: no spills)
+#pragma unroll
+          for (int r = 0; r < KR; ++r)
+            sm.wpart[mix][wave][r][lane] = make_double2(lacc[mix][r].m, lacc[mix][r].s);
+        }
       } else {
         erf_chunks<KR, LOGN, CENSUS>(uniform_ptr(cm), wv, K, ub, lb, valid, wlo, whi, exact, pacc[mix], cen);
       }
@@ -721,13 +727,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
         atomicAdd(A.census + 5, c2[1]);
       }
     }
-    if constexpr (WT) {
-      // the wave's sums are final: kept in registers for the finalize
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
-#pragma unroll
-        for (int r = 0; r < KR; ++r) wt_acc[q][r] = lacc[q][r];
-    } else {
+    if constexpr (!WT) {
 #pragma unroll
     for (int q = 0; q < 2; ++q)
 #pragma unroll
@@ -766,8 +766,8 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
     double lpb, lpa;
     if constexpr (LSE) {
       const double LN2 = 0.6931471805599453;
-      const double2 b = WT ? make_double2(wt_acc[0][r].m, wt_acc[0][r].s) : sm.merged[0][r][lane];
-      const double2 a = WT ? make_double2(wt_acc[1][r].m, wt_acc[1][r].s) : sm.merged[1][r][lane];
+      const double2 b = WT ? sm.wpart[0][wave][r][lane] : sm.merged[0][r][lane];
+      const double2 a = WT ? sm.wpart[1][wave][r][lane] : sm.merged[1][r][lane];
       lpb = (b.x == -INFINITY) ? NAN : (b.x + log2(b.y)) * LN2;
       lpa = (a.x == -INFINITY) ? NAN : (a.x + log2(a.y)) * LN2;
       if constexpr (LOGN) { const double lx = log(x[r]); lpb -= lx; lpa -= lx; }

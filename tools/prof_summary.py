@@ -61,7 +61,7 @@ def main(src, tag, config):
         summary[k] = e
     with open(os.path.join(out, '%s_%s_pmc.json' % (tag, config)), 'w') as f:
         json.dump(summary, f, indent=1, sort_keys=True)
-    tpath = os.path.join(out, 'traffic.json')
+    tpath = os.path.join(ROOT, 'traffic.json')
     traffic = json.load(open(tpath)) if os.path.exists(tpath) else {}
     traffic[config] = {'score': v['hbm_bytes'] for k, v in summary.items()
                        if k == 'k_score' and 'hbm_bytes' in v}
