@@ -32,9 +32,14 @@ class InvalidTrial(ValueError):
     """A document that does not have the trial layout (base.py:372-400)."""
 
 
+_PLAIN = (str, int, float, bool, type(None), datetime.datetime)
+
+
 def SONify(arg):
     """numpy scalars / arrays -> plain Python containers and numbers
     (the reference's BSON-friendliness pass, base.py:108-150)."""
+    if type(arg) in _PLAIN:  # the common leaves: one exact type test
+        return arg
     if isinstance(arg, dict):
         return {SONify(k): SONify(v) for k, v in arg.items()}
     if isinstance(arg, (list, tuple)):

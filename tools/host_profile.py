@@ -45,4 +45,4 @@ def main(cfg='cfg2', n=200):
 
 
 if __name__ == '__main__':
-    main(*sys.argv[1:])
+    main(sys.argv[1] if len(sys.argv) > 1 else "cfg2", int(sys.argv[2]) if len(sys.argv) > 2 else 200)
