@@ -424,10 +424,15 @@ def report(args, C, eng, world, mode, elapsed, value, pairs_step, pairs_suggest,
     lse_pairs = kinds.get('lse_gmm', 0.0) + kinds.get('lse_lgmm', 0.0)
     per_launch = max(1, launches)
     lse_exec = census[5] / per_launch if census[3] else lse_pairs
+    lse_shift = census[4] / per_launch if census[3] else 0.0   # of which one-exponent form
     erf_exec = census[2] / per_launch
     t_kernel = score_ms * 1e-3
-    t_peak = lse_exec / lse_peak + erf_exec / erf_peak
-    achieved = (lse_exec + erf_exec * lse_peak / erf_peak) / t_kernel if t_kernel else 0.0
+    # each evaluated pair priced at the register-only rate of the arithmetic
+    # it ran: per-group-max lift, one wave exponent, or quantized erf
+    t_peak = ((lse_exec - lse_shift) / lse_peak_exact + lse_shift / lse_peak_shift +
+              erf_exec / erf_peak)
+    frac = t_peak / t_kernel if t_kernel else None
+    achieved = (frac or 0.0) * lse_peak
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
@@ -439,15 +444,16 @@ def report(args, C, eng, world, mode, elapsed, value, pairs_step, pairs_suggest,
     lat_pairs_step = lat_pairs * (lat_launches / n_prof if n_prof else 0)
     eval_step = (lse_exec + erf_exec) * steps_per_launch + lat_pairs_step
     roof = dict(bound='valu', unit='Gpair/s', achieved=achieved / 1e9, peak=lse_peak / 1e9,
-                frac=(t_peak / t_kernel) if t_kernel else None, traffic=traffic,
+                frac=frac, traffic=traffic,
                 kernel='k_score (all lpdf kinds of a level, one launch)',
                 avg_launch_ms=score_ms, launches_per_step=steps_per_launch,
-                note='unit = log-sum-exp-pair equivalents: achieved = (evaluated LSE pairs + '
-                     'evaluated quantized pairs x lse_peak/erf_peak) / launch time; peaks are '
-                     'register-only microkernels of exactly the pair arithmetic (LSE pair: 2 '
-                     'fp64 FMA + cvt + v_exp_f32 + fp32/fp64 sum with the wave exponent folded '
-                     'into alpha, SURVEY 8d "1 exp + 6 flops" -- the faster of it and the '
-                     'per-group-max form; quantized pair: 2 OCML fp64 erf + 8 flops)',
+                note='frac = (time the evaluated pairs take at the register-only peak of the '
+                     'arithmetic each ran: per-group-max LSE pairs, one-wave-exponent LSE pairs, '
+                     'quantized erf pairs) / launch time; achieved = frac x peak, in pairs/s of '
+                     'the fastest (one-exponent) LSE form; peaks are microkernels of exactly the '
+                     'pair arithmetic (LSE pair: 2 fp64 FMA + cvt + v_exp_f32 + fp32/fp64 sum, '
+                     'SURVEY 8d "1 exp + 6 flops"; quantized pair: 2 OCML fp64 erf + 8 flops)',
+                lse_evaluated_shifted_pairs_per_launch=lse_shift,
                 lse_pairs_per_launch=lse_pairs, lse_evaluated_pairs_per_launch=lse_exec,
                 erf_pairs_per_launch=kinds.get('erf_gmm', 0.0) + kinds.get('erf_lgmm', 0.0),
                 erf_evaluated_pairs_per_launch=erf_exec,

@@ -515,8 +515,8 @@ class Plan(object):
 
     def census(self, enable):
         """Pair census since the last call: (quantized total, live, evaluated,
-        log-sum-exp total, 0, log-sum-exp evaluated); enable it for the
-        following suggests."""
+        log-sum-exp total, log-sum-exp evaluated in the one-exponent form,
+        log-sum-exp evaluated); enable it for the following suggests."""
         e = self.engine
         out = (C.c_int64 * 6)()
         with e.lock:

@@ -156,7 +156,7 @@ struct LseWindow {
 // Census of the log-sum-exp work (roofline accounting only): valid pairs and
 // the ones in evaluated (not skipped) blocks.
 struct LseCensus {
-  uint32_t total, exec;
+  uint32_t total, exec, shift;  // shift: the evaluated ones in the one-exponent form
 };
 
 // A block's envelope bound over the wave's candidate range [lo, hi]: the
@@ -332,6 +332,7 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
         }
         if (attempt == 0) cen.total += tot * (uint32_t)nvalid;
         cen.exec += ex * (uint32_t)nvalid;
+        cen.shift += ex * (uint32_t)nvalid;
       }
       uint64_t m0 = __ballot(live0), m1 = __ballot(live1);
       while (m0 | m1) {
@@ -647,7 +648,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
     // wave index as a scalar: the component addresses below are wave-uniform,
     // so the coefficients come in through scalar loads (SGPR operands)
     const int wv = __builtin_amdgcn_readfirstlane(wave);
-    LseCensus lcen{0u, 0u};
+    LseCensus lcen{0u, 0u, 0u};
     int nvalid = 0;
 #pragma unroll
     for (int r = 0; r < KR; ++r) nvalid += valid[r] ? 1 : 0;
@@ -716,14 +717,15 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
     }
     if constexpr (CENSUS && LSE) {
       // nvalid is per lane: the per-lane sums add up to the wave's pairs
-      unsigned long long c2[2] = {lcen.total, lcen.exec};
+      unsigned long long c2[3] = {lcen.total, lcen.exec, lcen.shift};
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
+      for (int q = 0; q < 3; ++q) {
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) c2[q] += __shfl_xor(c2[q], o, 64);
       }
       if (lane == 0) {
         atomicAdd(A.census + 3, c2[0]);
+        atomicAdd(A.census + 4, c2[2]);
         atomicAdd(A.census + 5, c2[1]);
       }
     }
