@@ -280,24 +280,55 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
   const int lane = threadIdx.x & 63;
   const int nch = (nb + kChunk - 1) / kChunk;
   const double *tb = reinterpret_cast<const double *>(cv);
-  // pass 1: the largest live block bound of the wave's chunks
+  // pass 1: the largest live block bound of the wave's chunks, and the block
   float bmax = -INFINITY;
+  int barg = -1;
   for (int r0 = c0; r0 < nch; r0 += STRIDE * 64) {
     const int c = r0 + STRIDE * lane;
     const int k0 = c * kChunk;
     if (c < nch) {
       const float b0 = envelope_bound(*reinterpret_cast<const float4 *>(tb + coef_off(k0, 3)), win);
-      if (b0 >= win.thr) bmax = fmaxf(bmax, b0);
+      if (b0 >= win.thr && b0 > bmax) { bmax = b0; barg = k0; }
       if (k0 + kGroup < nb) {
         const float b1 =
             envelope_bound(*reinterpret_cast<const float4 *>(tb + coef_off(k0 + kGroup, 3)), win);
-        if (b1 >= win.thr) bmax = fmaxf(bmax, b1);
+        if (b1 >= win.thr && b1 > bmax) { bmax = b1; barg = k0 + kGroup; }
       }
     }
   }
+  float wmax = bmax;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) bmax = fmaxf(bmax, __shfl_xor(bmax, o, 64));
-  if (!(bmax > -INFINITY && bmax < INFINITY)) return false;  // non-finite envelope
+  for (int o = 32; o > 0; o >>= 1) wmax = fmaxf(wmax, __shfl_xor(wmax, o, 64));
+  if (!(wmax > -INFINITY && wmax < INFINITY)) return false;  // non-finite envelope
+  {
+    // a tighter skip threshold: every lane's largest term is at least its
+    // largest term in the block of the highest bound (exact t, log2 units),
+    // usually several units above the probe's (the wide prior) that
+    // lse_window started from; the skip bound then holds as before
+    const uint64_t at = __ballot(bmax == wmax && barg >= 0);
+    const int kb = __shfl(barg, at ? __builtin_ctzll(at) : 0, 64);
+    if (kb >= 0) {
+      CoefGroup g;
+      load_group(cs, __builtin_amdgcn_readfirstlane(kb), g);
+      double lo = INFINITY;
+#pragma unroll
+      for (int r = 0; r < KR; ++r) {
+        if (!valid[r]) continue;
+        double mx = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < kGroup; ++j)
+          mx = fmax(mx, fma(g.z[j], y[r] * y[r], fma(g.y[j], y[r], g.x[j])));
+        lo = fmin(lo, mx);
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) lo = fmin(lo, __shfl_xor(lo, o, 64));
+      const float dead = kLseDeadBase + (float)(32 - __builtin_clz((unsigned)max(nb - 1, 1)));
+      const float t2 = (float)(lo - (double)dead) - 1.0f;
+      if (lo > -1.0e30 && lo < 1.0e30 && t2 > win.thr)
+        win.thr = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, t2)));
+    }
+  }
+  bmax = wmax;
   // pass 2 with M = ceil(bmax) + 1 for every lane; a lane whose sum comes
   // out below 2^-4 re-centres on its own sum (M + ceil(log2 s) + 1, the sum
   // then in (1/4, 1/2]) and the wave runs once more; failing that (or a sum

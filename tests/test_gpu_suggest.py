@@ -480,3 +480,44 @@ def _graph_threshold_body():
         want = plan.suggest([seed], 512)
         assert np.isfinite(got['value'][got['active'] == 1]).all(), i
         np.testing.assert_array_equal(got.view(np.uint8), want.view(np.uint8), err_msg=str(i))
+
+
+def test_sorted_draw_suggest_is_reproducible():
+    """Large draws come out value-bucketed with a stable (thread-timing
+    independent) scatter, so the pruned wave tiles see the same candidate
+    windows every run: the same suggest twice is identical bit for bit."""
+    meta, d, dom, trials = _fixture_trials('cfg2')
+    tpe.suggest([meta['new_id']], dom, trials, 7, n_EI_candidates=64)
+    plan = dom._tpe_state.plan
+    n = 1 << 18                       # 2^18 x 20 hps: the sorted-draw path
+    a = plan.suggest([31, 32], n)
+    b = plan.suggest([31, 32], n)
+    np.testing.assert_array_equal(a.view(np.uint8), b.view(np.uint8))
+
+
+def test_small_draw_pruning_in_child_process():
+    """Opt-in bucketing + block skip of small-draw log-sum-exp slots
+    (TPE_SMALL_SORT=1, read once per process): batched suggestions equal the
+    single-seed ones bit for bit, and the winners equal the default path's up
+    to near-ties (the skip moves an lpdf by <= 2^-30 relative)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys, numpy as np; sys.path.insert(0, 'tests'); import test_gpu_suggest as t; "
+            "t.test_batched_suggest_equals_single_seed_suggests(); "
+            "meta, d, dom, trials = t._fixture_trials('cfg2'); "
+            "t.tpe.suggest([meta['new_id']], dom, trials, 7, n_EI_candidates=64); "
+            "r = dom._tpe_state.plan.suggest([5, 6], 8192); "
+            "np.save(sys.argv[1], r); print('OK')")
+    import tempfile
+    with tempfile.TemporaryDirectory() as td:
+        out = [os.path.join(td, 'on.npy'), os.path.join(td, 'off.npy')]
+        for path, flag in zip(out, ('1', '0')):
+            r = subprocess.run([sys.executable, '-c', code, path], cwd=root,
+                               env=dict(os.environ, TPE_SMALL_SORT=flag),
+                               capture_output=True, text=True, timeout=300)
+            assert r.returncode == 0 and 'OK' in r.stdout, (r.stdout[-1000:], r.stderr[-3000:])
+        on, off = np.load(out[0]), np.load(out[1])
+    from gpu_util import assert_winners_match
+    assert_winners_match(on, off, msg='small-draw pruning')
