@@ -464,7 +464,9 @@ def report(args, C, eng, world, mode, elapsed, value, pairs_step, pairs_suggest,
     if lat_launches:
         roof['lattice'] = dict(
             kernel='k_lattice (bounded quantized hps: every lattice value j*q scored once per '
-                   'call; candidates look their lpdfs up in k_score; bit-identical)',
+                   'call; candidates look their lpdfs up in k_score; bit-identical); for small '
+                   'draws the launch also carries the candidate-draw rows (k_lattice<true>), '
+                   'so its time includes the draw',
             avg_launch_ms=lat_ms, launches_per_step=lat_launches / n_prof,
             pairs_per_launch=lat_pairs)
     ms_step = 1e3 * elapsed / args.steps
