@@ -1003,6 +1003,21 @@ void k_score(ScoreArgs A) {
 // sums of the below / above mixture in erf_chunks' canonical order (chunk c
 // to the total of "wave" c mod kWaves, totals in wave order), so a lattice
 // lpdf is bit-identical to the per-candidate kernel's for that value.
+// pc + v[lane + 1] + v[lane + 2] + ... + v[lane + I] in that order, the
+// neighbours read with DPP row_shl (within the lane's 16-lane row; no LDS
+// round trip per term)
+template <int I>
+struct RowShlSum {
+  static __device__ __forceinline__ double run(double pc, double v) {
+    static_assert(I < 16, "row_shl reaches 15 lanes");
+    return RowShlSum<I - 1>::run(pc, v) + dppd<0x100 + I>(v);
+  }
+};
+template <>
+struct RowShlSum<0> {
+  static __device__ __forceinline__ double run(double pc, double) { return pc; }
+};
+
 template <bool LOGN>
 __device__ __forceinline__ void lattice_point(const ScoreArgs &A, const tpe_hp &H, int hp,
                                               const LatInfo &L, int64_t pt, double *csum,
@@ -1017,7 +1032,7 @@ __device__ __forceinline__ void lattice_point(const ScoreArgs &A, const tpe_hp &
   const int nch = ncb + nca;
   const double *cb = reinterpret_cast<const double *>(A.coef + sb * A.kcap);
   const double *ca = reinterpret_cast<const double *>(A.coef + (sb + 1) * A.kcap);
-  const int seg = (threadIdx.x & 63) & ~(kChunk - 1), j = threadIdx.x & (kChunk - 1);
+  const int j = threadIdx.x & (kChunk - 1);
   // kLatU rounds of the block at a time: every coefficient load of the batch
   // is issued before the first erf, so one memory latency covers kLatU rounds
   constexpr int kLatU = 4;
@@ -1043,9 +1058,9 @@ __device__ __forceinline__ void lattice_point(const ScoreArgs &A, const tpe_hp &
         const double zu = (ub - cx[u]) * cy[u], zl = (lb - cx[u]) * cy[u];
         if (!erf_dead(zu, zl)) inc = erf_term<LOGN>(zu, zl, cw[u]);
       }
-      double pc = 0.0;  // the chunk in component order
-#pragma unroll
-      for (int i = 0; i < kChunk; ++i) pc += __shfl(inc, seg + i, 64);
+      // the chunk in component order, summed in its first lane: lane seg
+      // reads lane seg + i of its 16-lane DPP row (row_shl:i)
+      const double pc = RowShlSum<kChunk - 1>::run(0.0 + inc, inc);
       if (j == 0 && c < nch) csum[c] = pc;
     }
   }
@@ -1060,12 +1075,8 @@ __device__ __forceinline__ void lattice_point(const ScoreArgs &A, const tpe_hp &
     const int c0 = above ? ncb : 0, n = above ? nca : ncb;
     for (int c = w; c < n; c += kWaves) sw += csum[c0 + c];
   }
-  double tot = sw;
-#pragma unroll
-  for (int w = 1; w < kWaves; ++w) {
-    const double v = __shfl(sw, (t & ~(kWaves - 1)) + w, 64);
-    tot = tot + v;
-  }
+  static_assert(kWaves == 8, "the wave totals of a mixture sit in 8 lanes of one DPP row");
+  const double tot = RowShlSum<kWaves - 1>::run(sw, sw);
   if (t == 0 || t == kWaves) {
     const int above = t / kWaves;
     const double lp = log(tot) - (above ? ia.log_pacc : ib.log_pacc);
