@@ -231,83 +231,6 @@ __device__ __forceinline__ void lse_chunks(KDbl *__restrict__ cs, const Coef *__
   }
 }
 
-// The same exact loop for a wave tile, all chunks by one wave in the 8-wave
-// tile's association -- chunk owner v = c (mod kWaves) summed as its own
-// pass, the passes merged in owner order, so the sums are bit-identical to
-// lse_chunks<KR, CENSUS, kWaves>(c0 = v) merged over v -- but with ONE
-// envelope scan: lane l tests chunks l and 64 + l (nb <= 2048 components),
-// and pass v walks the live bits j = v (mod 8) of those two masks.
-template <int KR, bool CENSUS>
-__device__ __forceinline__ void lse_chunks_owners(KDbl *__restrict__ cs,
-                                                  const Coef *__restrict__ cv, int nb,
-                                                  const double (&y)[KR], LseAcc (&out)[KR],
-                                                  bool prune, LseWindow win, int nvalid,
-                                                  LseCensus &cen) {
-  const int lane = threadIdx.x & 63;
-  const int nch = (nb + kChunk - 1) / kChunk;  // <= 128
-  uint64_t M0[2], M1[2];
-#pragma unroll
-  for (int rd = 0; rd < 2; ++rd) {
-    const int c = 64 * rd + lane;
-    const int k0 = c * kChunk;
-    const bool has0 = c < nch, has1 = has0 && k0 + kGroup < nb;
-    bool live0 = has0, live1 = has1;
-    if (prune && has0) {
-      const double *t = reinterpret_cast<const double *>(cv);
-      live0 = envelope_bound(*reinterpret_cast<const float4 *>(t + coef_off(k0, 3)), win) >= win.thr;
-      if (has1)
-        live1 = envelope_bound(*reinterpret_cast<const float4 *>(t + coef_off(k0 + kGroup, 3)),
-                               win) >= win.thr;
-    }
-    if constexpr (CENSUS) {
-      const int n0 = has0 ? min(kGroup, nb - k0) : 0, n1 = has1 ? min(kGroup, nb - k0 - kGroup) : 0;
-      uint32_t tot = (uint32_t)(n0 + n1), ex = (uint32_t)((live0 ? n0 : 0) + (live1 ? n1 : 0));
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        tot += __shfl_xor(tot, o, 64);
-        ex += __shfl_xor(ex, o, 64);
-      }
-      cen.total += tot * (uint32_t)nvalid;
-      cen.exec += ex * (uint32_t)nvalid;
-    }
-    M0[rd] = __ballot(live0);
-    M1[rd] = __ballot(live1);
-  }
-  double y2[KR];
-#pragma unroll
-  for (int r = 0; r < KR; ++r) y2[r] = y[r] * y[r];
-  for (int v = 0; v < kWaves; ++v) {
-    double m[KR], s[KR];
-#pragma unroll
-    for (int r = 0; r < KR; ++r) { m[r] = -INFINITY; s[r] = 0.0; }
-    const uint64_t own = 0x0101010101010101ull << v;  // chunks j = v (mod 8) of a round
-#pragma unroll
-    for (int rd = 0; rd < 2; ++rd) {
-      uint64_t m0 = M0[rd] & own, m1 = M1[rd] & own;
-      while (m0 | m1) {
-        const int j0 = m0 ? __builtin_ctzll(m0) : 64, j1 = m1 ? __builtin_ctzll(m1) : 64;
-        const int g = j1 < j0 ? 1 : 0;
-        const int j = g ? j1 : j0;
-        if (g) m1 &= m1 - 1;
-        else m0 &= m0 - 1;
-        const int kg = (64 * rd + j) * kChunk + g * kGroup;
-        CoefGroup cgp;
-        load_group(cs, kg, cgp);
-        lse_group<KR, false>(cgp, kg, nb, y, y2, m, s);
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < KR; ++r) {
-      LseAcc part;
-      if (y[r] != y[r]) part = LseAcc{NAN, NAN};
-      else if (m[r] == -INFINITY) part = s[r] == 0.0 ? LseAcc{-INFINITY, 0.0} : LseAcc{NAN, NAN};
-      else part = LseAcc{m[r], s[r]};
-      if (v == 0) out[r] = part;
-      else lse_merge(out[r], part);
-    }
-  }
-}
-
 // Shifted log-sum-exp over the live blocks (value-bucketed tiles): one
 // exponent M for the whole wave instead of a per-group max and lift.  M =
 // ceil(largest live block bound over the wave's range) + 1 is an upper bound
@@ -784,10 +707,6 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
                                                                 lcen);
         if (!shifted) {
           if constexpr (WT) {
-            if (K <= 2 * 64 * kChunk) {
-              lse_chunks_owners<KR, CENSUS>(uniform_ptr(cm), cm, K, y, lacc[mix], prune, win,
-                                            nvalid, lcen);
-            } else
             // the exact loop in the 8-wave tile's association: chunk owner
             // v = c (mod kWaves) as 8 passes, merged in owner order -- the
             // same sums, bit for bit, as the component-split tile's waves
