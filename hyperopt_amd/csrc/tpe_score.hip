@@ -889,6 +889,24 @@ namespace tpe {
 // slots cut into tiles of 64 * tile_rows(kind) candidates (1 row for the
 // quantized kinds, whose per-pair cost is highest: smaller blocks spread their
 // work over more CUs; 2 for log-sum-exp; 4 for categorical lookups).
+// XCD-aware tile order inside a kind group.  Workgroups are dispatched to the
+// 8 XCDs round-robin by flat id, each XCD with its own L2: local block l of a
+// group of n (the first of which sits on XCD p) runs on XCD (p + l) % 8.
+// Renumber so that every XCD takes one contiguous run of the group's tiles
+// -- a slot's tiles then share one or two L2s (its coefficient tables are
+// fetched by those only, not by all 8), and every XCD still gets the same
+// share of the group's work.
+__device__ __forceinline__ int xcd_local(int l, int n, int p) {
+  const int q = (p + l) & 7;               // this block's XCD
+  const int fq = (q - p + 8) & 7;          // the group's first local on XCD q
+  int off = 0;
+  for (int x = 0; x < q; ++x) {            // locals on the XCDs before q
+    const int fx = (x - p + 8) & 7;
+    off += fx < n ? (n - fx + 7) >> 3 : 0;
+  }
+  return off + ((l - fq) >> 3);
+}
+
 template <bool ERFK, bool CENSUS>
 __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(6)))
 void k_score(ScoreArgs A) {
@@ -896,7 +914,9 @@ void k_score(ScoreArgs A) {
   const int b = blockIdx.x;
   int g = 0;
   while (g + 1 < A.n_groups && b >= A.grp_block0[g + 1]) ++g;
-  const int local = b - A.grp_block0[g], nt = A.grp_tiles[g];
+  const int nt = A.grp_tiles[g];
+  const int local = xcd_local(b - A.grp_block0[g], A.grp_block0[g + 1] - A.grp_block0[g],
+                              (int)(((int64_t)blockIdx.y * gridDim.x + A.grp_block0[g]) & 7));
   const int slot = A.grp_slot0[g] + local / nt, tile = local % nt;
   switch (A.grp_kind[g]) {
     case KIND_LSE_G: score_tile<KIND_LSE_G, CENSUS>(A, sm, slot, tile, nt); break;
