@@ -25,6 +25,7 @@ using namespace tpe;
 static int lse_shift_min();
 static bool wave_tiles_on();
 static bool small_sort_on();
+static int64_t chunk_budget();
 constexpr int64_t kSmallSortMin = 2048;  // candidates per chunk worth bucketing a small draw
 
 struct tpe_engine {
@@ -551,7 +552,7 @@ int score_launch(tpe_engine *h, tpe_plan *p, ScoreArgs a, bool has_erf, int64_t 
 
 // One level of conditional hps: one draw(+bucket) launch and one scoring
 // launch (every lpdf kind) for all of its hps.  Candidates are processed in
-// chunks so the buffer stays <= 512 MB.
+// chunks so the buffer stays <= 2 GB (chunk_budget).
 int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_cand,
               int64_t cand_begin, hipStream_t st) {
   const int32_t n_level = (int32_t)p->levels[level].size();
@@ -580,7 +581,7 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
   const bool lat_level = n_lat > 0 && p->lattice_on && rmax <= n_cand * n_sug &&
                          2 * ((p->kcap + 15) / 16) <= (int64_t)kLatChunks;
   if (!lat_level) n_lat = 0;
-  const int64_t budget = (int64_t)64 << 20;  // doubles
+  const int64_t budget = chunk_budget();  // doubles
   const int64_t chunk = std::max<int64_t>(
       1, std::min<int64_t>(std::max<int64_t>(n_cand, 1),
                            budget / std::max<int64_t>(1, n_sug * n_level)));
@@ -1548,6 +1549,15 @@ static bool small_sort_on() {
   static const bool v = [] {
     const char *e = std::getenv("TPE_SMALL_SORT");
     return e && std::atoi(e) != 0;
+  }();
+  return v;
+}
+
+// candidate buffer per scoring chunk, in doubles (TPE_CHUNK_MB overrides, A/B)
+static int64_t chunk_budget() {
+  static const int64_t v = [] {
+    const char *e = std::getenv("TPE_CHUNK_MB");
+    return (e ? std::atoll(e) : 2048) << 17;  // MB -> doubles (2 GB: 1 % faster than 512 MB at config 4, 2 % at config 5)
   }();
   return v;
 }
