@@ -244,8 +244,9 @@ int tpe_plan_set_lattice(tpe_plan_t p, int32_t enable);
  * scoring work since the last call -- counts[0] valid quantized (candidate,
  * component) pairs, [1] live ones (not an exact zero), [2] quantized pairs
  * evaluated (live for some lane of their wave), [3] valid log-sum-exp pairs,
- * [4] reserved (0), [5] log-sum-exp pairs evaluated (outside the component
- * blocks skipped as exact zeros) -- and switch the census on (enable != 0)
+ * [4] of [5] the ones evaluated in the one-exponent-per-wave form, [5]
+ * log-sum-exp pairs evaluated (outside the component blocks skipped as exact
+ * zeros; a wave's retried pass counts again) -- and switch the census on (enable != 0)
  * or off for the following suggests.  counts has 6 entries.               */
 int tpe_plan_census(tpe_plan_t p, int32_t enable, int64_t *counts);
 
