@@ -424,8 +424,15 @@ __device__ __forceinline__ void block_np_sums(const double *const (&arr)[NA], in
   const int s = threadIdx.x & 7, groups = blockDim.x >> 3;
   for (int64_t c0 = 0; c0 < n; c0 += 8192) {
     const int cn = (int)min<int64_t>(8192, n - c0);
+    // a node at depth d holds at most cn / 2^d + 16 elements (a right child
+    // is at most 7 above half its parent), so internal nodes (> 128) live at
+    // depth <= dtop and leaves below heap id 2^(dtop + 2)
+    int dtop = 0;
+    while (dtop < 6 && cn > (112 << (dtop + 1))) ++dtop;
+    const int idend = 1 << (dtop + 2);
     __syncthreads();  // previous chunk's root consumed, the arrays written
-    for (int id0 = 1; id0 < kNpHeap; id0 += groups) {  // uniform trip count
+    STAMP(28);
+    for (int id0 = 1; id0 < idend; id0 += groups) {  // uniform trip count
       const int id = id0 + (threadIdx.x >> 3);
       const NpNode nd = id < kNpHeap ? np_node(cn, id) : NpNode{0, 0};
       const bool leaf = nd.n > 0 && nd.n <= 128;
@@ -448,22 +455,23 @@ __device__ __forceinline__ void block_np_sums(const double *const (&arr)[NA], in
         r = r + dppd<kDppXor2>(r);
         r = r + dppd<kDppHalfMirror>(r);
         if (leaf && s == 0) {
-          double res;
-          if (ln < 8) {
-            res = 0.0;
-            for (int i = 0; i < ln; ++i) res += p[i];
-          } else {
-            res = r;
-            for (int i = body; i < ln; ++i) res += p[i];
-          }
+          // the (< 8) trailing elements in order: loads first, then the adds
+          const int t0 = ln < 8 ? 0 : body;
+          double res = ln < 8 ? 0.0 : r, tl[7];
+#pragma unroll
+          for (int j = 0; j < 7; ++j) tl[j] = (t0 + j < ln) ? p[t0 + j] : 0.0;
+#pragma unroll
+          for (int j = 0; j < 7; ++j)
+            if (t0 + j < ln) res += tl[j];
           sm.val[q][id] = res;
         }
       }
     }
     __syncthreads();
+    STAMP(29);
     if (threadIdx.x < 64) {
       const int lane = threadIdx.x;
-      for (int d = 6; d >= 0; --d) {  // internal nodes live at depth <= 6
+      for (int d = dtop; d >= 0; --d) {
         const int id = (1 << d) + lane;
         if (lane < (1 << d) && np_node(cn, id).n > 128) {
 #pragma unroll
