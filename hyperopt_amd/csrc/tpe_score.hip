@@ -107,23 +107,25 @@ __device__ __forceinline__ void load_group(KDbl *__restrict__ cs, int k, CoefGro
 // reaches the lpdf as the reference's NaN (logsum_rows, tpe.py:37-40); fmax
 // drops it from the exponent, so a lane whose terms are all NaN keeps
 // m = -inf and scores NaN as well.
-template <int KR, bool TAIL>
-__device__ __forceinline__ void lse_group(const CoefGroup &g, int k, int nb,
-                                          const double (&y)[KR], const double (&y2)[KR],
-                                          double (&m)[KR], double (&s)[KR]) {
+template <int KR>
+__device__ __forceinline__ void lse_terms(const CoefGroup &g, const double (&y)[KR],
+                                          const double (&y2)[KR], double (&t)[KR][kGroup]) {
+#pragma unroll
+  for (int r = 0; r < KR; ++r)
+#pragma unroll
+    for (int j = 0; j < kGroup; ++j)
+      // alpha + beta y' + gamma y'^2, one scalar coefficient per FMA
+      t[r][j] = fma(g.z[j], y2[r], fma(g.y[j], y[r], g.x[j]));
+}
+template <int KR>
+__device__ __forceinline__ void lse_fold(const double (&t)[KR][kGroup], double (&m)[KR],
+                                         double (&s)[KR]) {
 #pragma unroll
   for (int r = 0; r < KR; ++r) {
-    double t[kGroup];
-#pragma unroll
-    for (int j = 0; j < kGroup; ++j) {
-      // alpha + beta y' + gamma y'^2, one scalar coefficient per FMA
-      t[j] = fma(g.z[j], y2[r], fma(g.y[j], y[r], g.x[j]));
-      if (TAIL && k + j >= nb) t[j] = -INFINITY;  // wave-uniform
-    }
     // group max as a tree (fmax drops NaN terms)
     double mx[kGroup];
 #pragma unroll
-    for (int j = 0; j < kGroup; ++j) mx[j] = t[j];
+    for (int j = 0; j < kGroup; ++j) mx[j] = t[r][j];
 #pragma unroll
     for (int w = kGroup / 2; w > 0; w >>= 1)
 #pragma unroll
@@ -137,13 +139,27 @@ __device__ __forceinline__ void lse_group(const CoefGroup &g, int k, int nb,
     // terms 2^(t - m) <= 1 summed as an fp32 tree (<= kGroup), then in fp64
     float e[kGroup];
 #pragma unroll
-    for (int j = 0; j < kGroup; ++j) e[j] = __builtin_amdgcn_exp2f((float)(t[j] - ms));
+    for (int j = 0; j < kGroup; ++j) e[j] = __builtin_amdgcn_exp2f((float)(t[r][j] - ms));
 #pragma unroll
     for (int w = kGroup / 2; w > 0; w >>= 1)
 #pragma unroll
       for (int j = 0; j < w; ++j) e[j] += e[j + w];
     s[r] += (double)e[0];
   }
+}
+
+// the next live block of a round (chunk j's block 0 before its block 1
+// before chunk j + 1): its first component, popped from the masks
+template <int STRIDE>
+__device__ __forceinline__ bool next_live(uint64_t &m0, uint64_t &m1, int r0, int &kg) {
+  if (!(m0 | m1)) return false;
+  const int j0 = m0 ? __builtin_ctzll(m0) : 64, j1 = m1 ? __builtin_ctzll(m1) : 64;
+  const int g = j1 < j0 ? 1 : 0;
+  const int j = g ? j1 : j0;
+  if (g) m1 &= m1 - 1;
+  else m0 &= m0 - 1;
+  kg = (r0 + STRIDE * j) * kChunk + g * kGroup;
+  return true;
 }
 
 // The wave's pruning window for one mixture (lse_chunks' PRUNE mode): the
@@ -211,16 +227,21 @@ __device__ __forceinline__ void lse_chunks(KDbl *__restrict__ cs, const Coef *__
     // live blocks in order: chunk j's block 0 before its block 1 before chunk
     // j + 1 (the padding components of a last block have alpha = -inf,
     // make_coef_pad, so no tail masking is needed)
-    while (m0 | m1) {
-      const int j0 = m0 ? __builtin_ctzll(m0) : 64, j1 = m1 ? __builtin_ctzll(m1) : 64;
-      const int g = j1 < j0 ? 1 : 0;
-      const int j = g ? j1 : j0;
-      if (g) m1 &= m1 - 1;
-      else m0 &= m0 - 1;
-      const int kg = (r0 + STRIDE * j) * kChunk + g * kGroup;
-      CoefGroup cgp;
-      load_group(cs, kg, cgp);
-      lse_group<KR, false>(cgp, kg, nb, y, y2, m, s);
+    // software-pipelined: the next live block's coefficients are loaded into
+    // the same scalar registers once this block's terms are formed, so the
+    // load overlaps the block's max / exp / sum (scalar loads complete out of
+    // order, so only one batch may be in flight)
+    int kg = 0;
+    bool have = next_live<STRIDE>(m0, m1, r0, kg);
+    CoefGroup cgp;
+    if (have) load_group(cs, kg, cgp);
+    while (have) {
+      double t[KR][kGroup];
+      lse_terms<KR>(cgp, y, y2, t);
+      have = next_live<STRIDE>(m0, m1, r0, kg);  // (kg kept after the last)
+      load_group(cs, kg, cgp);  // unconditional: no branch merge of the registers
+      __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of the fold
+      lse_fold<KR>(t, m, s);
     }
   }
 #pragma unroll
@@ -245,30 +266,33 @@ __device__ __forceinline__ void lse_chunks(KDbl *__restrict__ cs, const Coef *__
 // alpha - M)): each FMA reads one scalar (SGPR) coefficient, so no VALU move
 // of a second one is needed (one scalar operand per VALU instruction).
 template <int KR>
-__device__ __forceinline__ void lse_group_shifted(const CoefGroup &g, double M,
+__device__ __forceinline__ void lse_terms_shifted(const CoefGroup &g, double M,
                                                   const double (&y)[KR], const double (&y2)[KR],
-                                                  double (&s)[KR]) {
-  // two halves of 4 components: the shifted alphas and the fp32 terms of a
-  // half stay in few VGPRs; a lane's group sum is (h0 tree) + (h1 tree)
-  float f[KR];
+                                                  float (&d)[KR][kGroup]) {
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     double am[kGroup / 2];
 #pragma unroll
     for (int j = 0; j < kGroup / 2; ++j) am[j] = g.x[4 * h + j] - M;
 #pragma unroll
-    for (int r = 0; r < KR; ++r) {
-      float e[kGroup / 2];
+    for (int r = 0; r < KR; ++r)
 #pragma unroll
       for (int j = 0; j < kGroup / 2; ++j)
-        e[j] = __builtin_amdgcn_exp2f(
-            (float)fma(g.z[4 * h + j], y2[r], fma(g.y[4 * h + j], y[r], am[j])));
-      const float t = (e[0] + e[2]) + (e[1] + e[3]);
-      f[r] = h ? f[r] + t : t;
-    }
+        d[r][4 * h + j] = (float)fma(g.z[4 * h + j], y2[r], fma(g.y[4 * h + j], y[r], am[j]));
   }
+}
+// a lane's group sum is (h0 tree) + (h1 tree) over the halves of 4 components
+template <int KR>
+__device__ __forceinline__ void lse_fold_shifted(const float (&d)[KR][kGroup], double (&s)[KR]) {
 #pragma unroll
-  for (int r = 0; r < KR; ++r) s[r] += (double)f[r];
+  for (int r = 0; r < KR; ++r) {
+    float e[kGroup];
+#pragma unroll
+    for (int j = 0; j < kGroup; ++j) e[j] = __builtin_amdgcn_exp2f(d[r][j]);
+    const float t0 = (e[0] + e[2]) + (e[1] + e[3]);
+    const float t1 = (e[4] + e[6]) + (e[5] + e[7]);
+    s[r] += (double)(t0 + t1);
+  }
 }
 
 template <int KR, bool CENSUS, int STRIDE = kWaves>
@@ -366,15 +390,18 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
         cen.shift += ex * (uint32_t)nvalid;
       }
       uint64_t m0 = __ballot(live0), m1 = __ballot(live1);
-      while (m0 | m1) {
-        const int j0 = m0 ? __builtin_ctzll(m0) : 64, j1 = m1 ? __builtin_ctzll(m1) : 64;
-        const int g = j1 < j0 ? 1 : 0;
-        const int j = g ? j1 : j0;
-        if (g) m1 &= m1 - 1;
-        else m0 &= m0 - 1;
-        CoefGroup cgp;
-        load_group(cs, (r0 + STRIDE * j) * kChunk + g * kGroup, cgp);
-        lse_group_shifted<KR>(cgp, M, y, y2, s);
+      // software-pipelined as in lse_chunks
+      int kg = 0;
+      bool have = next_live<STRIDE>(m0, m1, r0, kg);
+      CoefGroup cgp;
+      if (have) load_group(cs, kg, cgp);
+      while (have) {
+        float d[KR][kGroup];
+        lse_terms_shifted<KR>(cgp, M, y, y2, d);
+        have = next_live<STRIDE>(m0, m1, r0, kg);
+        load_group(cs, kg, cgp);
+        __builtin_amdgcn_sched_barrier(0);
+        lse_fold_shifted<KR>(d, s);
       }
     }
     bool ok = true;
