@@ -40,8 +40,12 @@ EXPORTS = (
     'tpe_plan_profile', 'tpe_plan_profile_read', 'tpe_microbench', 'tpe_plan_get_results',
     'tpe_plan_results_device', 'tpe_plan_census', 'tpe_plan_fit_suggest',
     'tpe_plan_set_lattice', 'tpe_plan_update_history', 'tpe_plan_set_prune',
-    'tpe_plan_sample_prior',
+    'tpe_plan_sample_prior', 'tpe_plan_score_candidates_sorted',
 )
+
+# include/tpe_engine.h TPE_SHARD_ALIGN: candidate splits at multiples of this
+# give byte-identical suggests (the large-draw value-bucketing block)
+SHARD_ALIGN = 4096
 
 
 class EngineUnavailable(RuntimeError):
@@ -138,6 +142,8 @@ def load_library(path: str = LIB_PATH):
                                                vp, i32, vp]),
             'tpe_plan_merge': (C.c_int, [vp, vp, i32, i32, vp, i32, vp]),
             'tpe_plan_score_candidates': (C.c_int, [vp, i32, _D, i64, _D, _D, C.POINTER(i64), _D]),
+            'tpe_plan_score_candidates_sorted': (C.c_int, [vp, i32, i32, _D, i64, _D, _D,
+                                                           C.POINTER(i64), _D]),
             'tpe_plan_last_stats': (C.c_int, [vp, _D, _D]),
             'tpe_plan_profile': (C.c_int, [vp, i32]),
             'tpe_plan_profile_read': (C.c_int, [vp, i32, _D, C.POINTER(i64), _D]),
@@ -473,14 +479,21 @@ class Plan(object):
                                          0 if host else 1, stream))
         return res
 
-    def score_candidates(self, hp, x):
+    def score_candidates(self, hp, x, sorted_mode=None):
+        """Below / above lpdf and argmax of given candidates of one hp with
+        the fitted mixtures.  sorted_mode None: each candidate scored on its
+        own (exact sums); 0 / 1 / 2: the large-draw production form
+        (tpe_plan_score_candidates_sorted: value-bucketed blocks, log-sum-exp
+        prune mode 0 / 1 / 2)."""
         e = self.engine
         x = _f64(x).ravel()
         lb, la = np.empty(x.size), np.empty(x.size)
         bi, bs = C.c_int64(-1), C.c_double(np.nan)
+        mode = -1 if sorted_mode is None else int(sorted_mode)
         with e.lock:
-            e.check(e.lib.tpe_plan_score_candidates(self.p, int(hp), _dp(x), x.size, _dp(lb),
-                                                    _dp(la), C.byref(bi), C.byref(bs)))
+            e.check(e.lib.tpe_plan_score_candidates_sorted(self.p, int(hp), mode, _dp(x), x.size,
+                                                           _dp(lb), _dp(la), C.byref(bi),
+                                                           C.byref(bs)))
         return lb, la, bi.value, bs.value
 
     def profile(self, capacity):

@@ -582,9 +582,13 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
                          2 * ((p->kcap + 15) / 16) <= (int64_t)kLatChunks;
   if (!lat_level) n_lat = 0;
   const int64_t budget = chunk_budget();  // doubles
-  const int64_t chunk = std::max<int64_t>(
+  int64_t chunk = std::max<int64_t>(
       1, std::min<int64_t>(std::max<int64_t>(n_cand, 1),
                            budget / std::max<int64_t>(1, n_sug * n_level)));
+  // several chunks: each a whole number of sorted-draw blocks, so the blocks
+  // (and with them every pruned log-sum-exp) sit at the same global candidate
+  // indices however [0, n) is chunked or sharded (TPE_SHARD_ALIGN)
+  if (chunk < n_cand) chunk = std::max<int64_t>(kSortedBlock, chunk / kSortedBlock * kSortedBlock);
   // a small one-chunk draw whose tables fit kFuseTab runs in extra blocks of
   // the lattice launch (both only need the fitted mixtures): one launch less
   // and the draw hidden behind the lattice points
@@ -717,13 +721,24 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
 }
 
 // Externally supplied candidates of one hp (parity / operator path).
+// sorted_mode < 0: every candidate scored on its own (exact sums, any
+// tiling); >= 0: the large-draw production form -- value-bucketed in
+// kSortedBlock blocks as k_draw_sorted writes them, log-sum-exp prune mode
+// sorted_mode on the tiles run_level picks for it.
 int run_external(tpe_engine *h, tpe_plan *p, int32_t hp, const double *ext, int64_t n,
-                 double *lb, double *la, hipStream_t st) {
-  const int kind = score_kind(p->hps[hp]);
+                 double *lb, double *la, hipStream_t st, int32_t sorted_mode = -1) {
+  int kind = score_kind(p->hps[hp]);
+  const bool sorted = sorted_mode >= 0;
+  if (sorted && sorted_mode > 1 && wave_tiles_on())
+    kind = kind == KIND_LSE_G ? KIND_LSE_GW : kind == KIND_LSE_L ? KIND_LSE_LW : kind;
   ScoreArgs grid{};
   const int32_t pstride = set_score_groups(grid, &kind, 1, n);
   int rc = ensure_suggest_state(h, p, 1, (size_t)p->P * pstride);
   if (rc) return rc;
+  if (sorted) {
+    rc = ensure_cand(h, p, (size_t)std::max<int64_t>(1, n));
+    if (rc) return rc;
+  }
   ScoreArgs a = base_args(p, 1);
   copy_groups(a, grid);
   a.cand = ext;
@@ -735,6 +750,14 @@ int run_external(tpe_engine *h, tpe_plan *p, int32_t hp, const double *ext, int6
   a.out_lb = lb;
   a.out_la = la;
   a.force_active = 1;
+  if (sorted) {
+    a.cand = p->d_cand;
+    CKH(launch_sort_ext(a, ext, p->d_cpos, st));
+    a.cand_pos = p->d_cpos;
+    a.lse_pos = 1;
+    a.lse_prune = sorted_mode;
+    a.lse_shift_min = lse_shift_min();
+  }
   return score_launch(h, p, a, kind == KIND_ERF_G || kind == KIND_ERF_L, n, st, false);
 }
 
@@ -1368,9 +1391,18 @@ int tpe_plan_merge(tpe_plan_t p, const tpe_result *gathered, int32_t world, int3
 int tpe_plan_score_candidates(tpe_plan_t p, int32_t hp, const double *x, int64_t n,
                               double *llik_b, double *llik_a, int64_t *best_index,
                               double *best_score) {
+  return tpe_plan_score_candidates_sorted(p, hp, -1, x, n, llik_b, llik_a, best_index,
+                                          best_score);
+}
+
+int tpe_plan_score_candidates_sorted(tpe_plan_t p, int32_t hp, int32_t mode, const double *x,
+                                     int64_t n, double *llik_b, double *llik_a,
+                                     int64_t *best_index, double *best_score) {
   if (!p) return TPE_E_INVALID;
   tpe_engine *h = p->eng;
-  if (hp < 0 || hp >= p->P || n < 0 || (n > 0 && !x)) return fail(h, TPE_E_INVALID, "bad args");
+  if (hp < 0 || hp >= p->P || n < 0 || (n > 0 && !x) || mode < -1 || mode > 2)
+    return fail(h, TPE_E_INVALID, "bad args");
+  if (n > (int64_t)INT32_MAX) return fail(h, TPE_E_INVALID, "too many candidates");
   if (best_index) *best_index = -1;
   if (best_score) *best_score = NAN;
   if (n == 0) return TPE_OK;
@@ -1387,7 +1419,7 @@ int tpe_plan_score_candidates(tpe_plan_t p, int32_t hp, const double *x, int64_t
   if (rc) return rc;
   CKH(hipMemcpyAsync(p->d_ext, x, n * 8, hipMemcpyHostToDevice, st));
   rc = run_external(h, p, hp, p->d_ext, n, llik_b ? p->d_lb : nullptr,
-                    llik_a ? p->d_la : nullptr, st);
+                    llik_a ? p->d_la : nullptr, st, mode);
   if (rc) return rc;
   tpe_result r;
   CKH(hipMemcpyAsync(&r, p->d_results + hp, sizeof(r), hipMemcpyDeviceToHost, st));

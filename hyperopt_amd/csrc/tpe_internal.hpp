@@ -254,6 +254,11 @@ hipError_t launch_draw(const ScoreArgs &a, bool table, hipStream_t st);
 constexpr int kSortedBlock = 4096;
 hipError_t launch_draw_sorted(const ScoreArgs &a, bool small_table, int32_t *pos_out,
                               hipStream_t st);
+static_assert(kSortedBlock == TPE_SHARD_ALIGN, "shard alignment is the sorted-draw block");
+// given candidates src[slot][n_cand] (one suggestion) bucketed exactly as
+// k_draw_sorted buckets its draws (tpe_plan_score_candidates_sorted)
+hipError_t launch_sort_ext(const ScoreArgs &a, const double *src, int32_t *pos_out,
+                           hipStream_t st);
 // slots slot_begin .. n_slots-1 (the lattice slots before them are not bucketed)
 hipError_t launch_bucket(const ScoreArgs &a, int32_t slot_begin, int32_t *pos_out, hipStream_t st);
 hipError_t launch_merge(const int32_t *level_hps, int32_t n_slots,

@@ -158,18 +158,24 @@ struct SortedDrawLds {
   double red[2][kDrawThreads / 64];
 };
 
-template <int CAP>
-__global__ __launch_bounds__(kDrawThreads) void k_draw_sorted(ScoreArgs A, int32_t *__restrict__ pos_out) {
-  __shared__ SortedDrawLds<CAP> L;
+// EXT (k_sort_ext): the block's values come from src[slot][n_cand] instead
+// of the draw (given candidates scored exactly as a large draw's are)
+template <int CAP, bool EXT>
+__device__ __forceinline__ void sorted_block(const ScoreArgs &A, int32_t *__restrict__ pos_out,
+                                             const double *__restrict__ src,
+                                             SortedDrawLds<CAP> &L) {
   const int slot = blockIdx.y, s = blockIdx.z;
   const int hp = A.level_hps[slot];
   const tpe_hp H = A.hps[hp];
-  if (!hp_active(H, A.results + (int64_t)s * A.n_hp, A.cond_parent, A.cond_branch)) return;
+  if (!A.force_active && !hp_active(H, A.results + (int64_t)s * A.n_hp, A.cond_parent, A.cond_branch))
+    return;
   const int64_t sb = 2 * (int64_t)hp;
   const double *bw = A.mw + sb * A.kcap, *bmu = A.mmu + sb * A.kcap, *bsg = A.msig + sb * A.kcap;
   const int K = A.info[sb].K;
-  const bool tab = K >= 1 && K <= CAP;
-  if (tab) build_table(H, K, bw, bmu, bsg, L.T);
+  const bool tab = !EXT && K >= 1 && K <= CAP;
+  if constexpr (!EXT) {
+    if (tab) build_table(H, K, bw, bmu, bsg, L.T);
+  }
   const uint64_t seed = suggestion_seed(A, s);
   const int64_t base = (int64_t)blockIdx.x * kSortedBlock;
   const int n = (int)min<int64_t>(kSortedBlock, A.n_cand - base);
@@ -183,8 +189,14 @@ __global__ __launch_bounds__(kDrawThreads) void k_draw_sorted(ScoreArgs A, int32
 #pragma unroll 1
   for (int i = t; i < n; i += kDrawThreads) {
     const uint64_t gi = (uint64_t)(A.cand_begin + base + i);
-    const double x = tab ? draw_table_ool<CAP>(A.hps + hp, K, bmu, bsg, &L.T, seed, gi, (uint32_t)hp)
-                         : draw_one_ool(A.hps + hp, A.info + sb, bw, bmu, bsg, seed, gi, (uint32_t)hp);
+    double x;
+    if constexpr (EXT) {
+      (void)gi; (void)seed; (void)bw;
+      x = src[(int64_t)slot * A.n_cand + base + i];
+    } else {
+      x = tab ? draw_table_ool<CAP>(A.hps + hp, K, bmu, bsg, &L.T, seed, gi, (uint32_t)hp)
+              : draw_one_ool(A.hps + hp, A.info + sb, bw, bmu, bsg, seed, gi, (uint32_t)hp);
+    }
     if (!bucket) {
       out[i] = x;
       continue;
@@ -220,6 +232,18 @@ __global__ __launch_bounds__(kDrawThreads) void k_draw_sorted(ScoreArgs A, int32
     out[p] = L.xs[i];
     po[p] = (int32_t)(base + i);
   });
+}
+
+template <int CAP>
+__global__ __launch_bounds__(kDrawThreads) void k_draw_sorted(ScoreArgs A, int32_t *__restrict__ pos_out) {
+  __shared__ SortedDrawLds<CAP> L;
+  sorted_block<CAP, false>(A, pos_out, nullptr, L);
+}
+
+__global__ __launch_bounds__(kDrawThreads) void k_sort_ext(ScoreArgs A, const double *__restrict__ src,
+                                                           int32_t *__restrict__ pos_out) {
+  __shared__ SortedDrawLds<1> L;
+  sorted_block<1, true>(A, pos_out, src, L);
 }
 
 // Bucket each 8192-candidate chunk of the erf-kind hps by value (counting
@@ -589,6 +613,14 @@ hipError_t launch_draw_sorted(const ScoreArgs &a, bool small_table, int32_t *pos
   const dim3 g(gx, a.n_slots, a.n_suggest);
   if (small_table) k_draw_sorted<kFuseTab><<<g, kDrawThreads, 0, st>>>(a, pos_out);
   else k_draw_sorted<kTabCap><<<g, kDrawThreads, 0, st>>>(a, pos_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_sort_ext(const ScoreArgs &a, const double *src, int32_t *pos_out,
+                           hipStream_t st) {
+  if (a.n_slots <= 0 || a.n_suggest != 1 || a.n_cand <= 0) return hipSuccess;
+  const unsigned gx = (unsigned)((a.n_cand + kSortedBlock - 1) / kSortedBlock);
+  k_sort_ext<<<dim3(gx, a.n_slots, 1), kDrawThreads, 0, st>>>(a, src, pos_out);
   return hipGetLastError();
 }
 

@@ -76,6 +76,7 @@ class TrialHistory(object):
         self.tids = []
         self.docs = []          # the document of each row
         self._row = {}          # id(doc) -> row (incremental mode)
+        self._dropped = {}      # id(doc) -> doc: visible documents without a row
         self._pending = set()   # rows with loss +inf (new / running / failed)
         self._owner = None      # weakref to the Trials synced
         self._epoch = None
@@ -161,6 +162,11 @@ class TrialHistory(object):
             if k in done:
                 continue
             done.add(k)
+            if k in self._dropped and self._dropped[k] is doc:
+                # a visible document the last rebuild left out (a first NaN
+                # loss, or a duplicate tid that lost the dedupe) changed: it
+                # may belong in the history now
+                return False
             r = self._row.get(k)
             if r is None or self.docs[r] is not doc:
                 continue                        # not a row (yet): appended below
@@ -220,6 +226,8 @@ class TrialHistory(object):
                 cur[0], cur[1] = loss, doc
         rows = sorted(((t, e[0], e[1]) for t, e in best.items() if e[1] is not None),
                       key=lambda z: z[0])
+        kept = {id(e[2]) for e in rows}
+        self._dropped = {id(d): d for d in view if id(d) not in kept}
         self._grow(len(rows))
         plain = True
         for r, (tid, loss, doc) in enumerate(rows):

@@ -30,16 +30,25 @@ from . import _engine as E
 RECORD_BYTES = E.RESULT_DTYPE.itemsize  # sizeof(tpe_result) == 32
 
 
-def shard_range(n: int, rank: int, world: int):
-    """(begin, count) of rank's share of [0, n): contiguous, balanced to
-    within one candidate, covering [0, n) exactly once over all ranks."""
+def shard_range(n: int, rank: int, world: int, align: int = 1):
+    """(begin, count) of rank's share of [0, n): contiguous, covering [0, n)
+    exactly once over all ranks, every boundary a multiple of ``align``
+    (balanced to within one unit of ``align``).  With
+    ``align=E.SHARD_ALIGN`` the shards' large draws are bucketed in the same
+    global blocks as the unsharded suggest's, so the merged result is byte
+    for byte the one-device result (include/tpe_engine.h TPE_SHARD_ALIGN)."""
     if world <= 0 or not 0 <= rank < world:
         raise ValueError('bad rank/world %r/%r' % (rank, world))
     if n < 0:
         raise ValueError('n < 0')
-    base, extra = divmod(n, world)
-    begin = rank * base + min(rank, extra)
-    return begin, base + (1 if rank < extra else 0)
+    if align < 1:
+        raise ValueError('align < 1')
+    units = -(-n // align)
+    base, extra = divmod(units, world)
+    u0 = rank * base + min(rank, extra)
+    u1 = u0 + base + (1 if rank < extra else 0)
+    begin, end = min(n, u0 * align), min(n, u1 * align)
+    return begin, end - begin
 
 
 def suggestion_slice(n_suggest: int, rank: int, world: int):
@@ -106,8 +115,13 @@ class ShardedSuggest(object):
     """One suggestion's candidates sharded over the ranks of ``group``.
 
     ``plan`` is this rank's :class:`hyperopt_amd._engine.Plan` (same space,
-    same history, fitted); the engine enqueues on torch's current stream so
-    the gather is ordered after the scoring and the merge after the gather.
+    same history).  Every engine call, record copy and collective runs on
+    one torch stream (``self.stream``), which waits on torch's current stream
+    at each call: fit the plan with :meth:`fit` (on that stream), or order a
+    fit made elsewhere before :meth:`suggest` yourself -- the engine's calls
+    are stream-ordered, not synchronous (include/tpe_engine.h).  Candidate
+    shards are aligned to ``E.SHARD_ALIGN``, so the merged winners are the
+    one-device winners byte for byte.
     """
 
     def __init__(self, plan, group=None):
@@ -124,11 +138,18 @@ class ShardedSuggest(object):
         self.stream = torch.cuda.Stream(self.device)
         self.gather = lambda t: gather_records(t, self.group)
 
+    def fit(self, **kw):
+        """tpe_plan_fit on the sharded stream (ordered before the next
+        :meth:`suggest`, after torch's current stream)."""
+        import torch
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        self.plan.fit(stream=self.stream.cuda_stream, **kw)
+
     def suggest(self, seeds, n_cand, fetch=True):
         import torch
         seeds = E._seeds(seeds)
         S, P = seeds.size, self.plan.n_hp
-        begin, count = shard_range(int(n_cand), self.rank, self.world)
+        begin, count = shard_range(int(n_cand), self.rank, self.world, E.SHARD_ALIGN)
         stream = self.stream.cuda_stream
         self.stream.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self.stream):

@@ -191,6 +191,22 @@ class _Store(object):
         self.keys = []
         self.journal.reset()
 
+    def __setstate__(self, state):
+        # a pickled / deep-copied store comes back with detached documents
+        # (TrialDoc.__reduce__): re-attach them, rebuild the state / key
+        # columns from the documents and start a new journal generation, so
+        # resuming fmin on an unpickled Trials tracks state changes again
+        # (the reference reads states from the documents, base.py:327-338)
+        self.__dict__.update(state)
+        self.state = _Column(np.int8, max(64, len(self.docs)))
+        self.keys = []
+        for r, doc in enumerate(self.docs):
+            doc._store = self
+            doc._row = r
+            self.state.push(_state_code(doc.get('state')))
+            self.keys.append(doc.get('exp_key'))
+        self.journal.reset()
+
 
 def _state_code(v):
     try:

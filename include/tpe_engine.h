@@ -25,6 +25,16 @@ extern "C" {
 
 #define TPE_ENGINE_ABI_VERSION 1
 
+/* Candidate-range alignment of bit-identical sharding: tpe_plan_suggest over
+ * [0, n) and over any split of [0, n) into ranges whose boundaries are
+ * multiples of TPE_SHARD_ALIGN (merged with tpe_plan_merge) give the same
+ * results byte for byte, as long as every part takes the same draw path (the
+ * large-draw value-bucketed path runs at >= 2^22 draws per call).  Large
+ * draws are value-bucketed in blocks of this many consecutive global
+ * candidate indices, and a candidate's pruned log-sum-exp depends on its
+ * block.  Unaligned splits still agree under the north-star tie rule. */
+#define TPE_SHARD_ALIGN 4096
+
 /* ---- status codes ---------------------------------------------------- */
 #define TPE_OK 0
 #define TPE_E_INVALID (-1)   /* bad argument / shape  -> TypeError/ValueError     */
@@ -150,7 +160,11 @@ int tpe_plan_num_levels(tpe_plan_t p, int32_t *n_levels);
 
 /* History in tid order (tpe.py:820-848): losses[n] (+inf for unfinished),
  * vals[n_hp][n], active[n_hp][n].  on_device != 0: pointers are device
- * memory (e.g. torch tensors); stream: hipStream_t or NULL.                */
+ * memory (e.g. torch tensors); stream: hipStream_t or NULL (the engine's).
+ * History updates are stream-ordered, not synchronous: the host buffers may
+ * be reused on return, but the device rows change in `stream`'s order, so a
+ * fit / suggest on another stream must be ordered after it by the caller
+ * (the same stream, or an event).  The same holds for every plan call. */
 int tpe_plan_set_history(tpe_plan_t p, const double *losses,
                          const double *vals, const uint8_t *active, int64_t n,
                          int32_t on_device, void *stream);
@@ -213,6 +227,18 @@ int tpe_plan_merge(tpe_plan_t p, const tpe_result *gathered, int32_t world,
 int tpe_plan_score_candidates(tpe_plan_t p, int32_t hp, const double *x,
                               int64_t n, double *llik_b, double *llik_a,
                               int64_t *best_index, double *best_score);
+
+/* The same, through the production scoring form of large draws: the given
+ * candidates are value-bucketed in blocks of TPE_SHARD_ALIGN exactly as
+ * k_draw_sorted buckets its draws, then scored on the same tiles with
+ * log-sum-exp prune mode `mode` (tpe_plan_set_prune: 0 every pair, 1 block
+ * skip, 2 block skip + one exponent per wave).  Outputs are in the given
+ * order.  The parity path of tpe.py:139-144 / 253-256 as the suggest
+ * computes it at config 4.                                                 */
+int tpe_plan_score_candidates_sorted(tpe_plan_t p, int32_t hp, int32_t mode,
+                                     const double *x, int64_t n, double *llik_b,
+                                     double *llik_a, int64_t *best_index,
+                                     double *best_score);
 
 /* Device time (ms) of the last tpe_plan_suggest, from HIP events on the
  * plan's stream (recorded only while tpe_plan_profile is on, else NaN: an

@@ -50,3 +50,9 @@ def test_struct_layouts_match_header():
     from hyperopt_amd import _engine as E
     assert ctypes.sizeof(E.TpeHp) == 72
     assert E.RESULT_DTYPE.itemsize == 32
+
+
+def test_shard_align_matches_header():
+    from hyperopt_amd import _engine as E
+    m = re.search(r'#define\s+TPE_SHARD_ALIGN\s+(\d+)', open(HEADER).read())
+    assert m and int(m.group(1)) == E.SHARD_ALIGN

@@ -275,3 +275,60 @@ def test_delete_all_and_refresh_cost_shape():
     t.insert_trial_docs(rand.suggest([9], dom, t, 7))
     t.refresh()
     assert t.tids == [9]
+
+
+def test_pickled_trials_resume_with_pending_doc():
+    """a Trials pickled with a queued NEW document comes
+    back with its documents attached to the store, so a resumed fmin sees
+    the evaluated state and finishes (the reference reads states from the
+    documents, base.py:327-338)."""
+    import signal
+    t = Trials()
+    H.fmin(lambda x: x ** 2, hp.uniform('x', -1, 1), algo=rand.suggest, max_evals=3, trials=t,
+           rstate=np.random.RandomState(0))
+    dom = Domain(lambda x: x ** 2, hp.uniform('x', -1, 1))
+    t.insert_trial_docs(rand.suggest(t.new_trial_ids(1), dom, t, 9))   # queued, never run
+    t.refresh()
+    for loaded in (pickle.loads(pickle.dumps(t)), copy.deepcopy(t)):
+        st = loaded._store
+        assert all(d._store is st and st.docs[d._row] is d for d in st.docs)
+        assert list(st.state.view()) == [d['state'] for d in st.docs]
+        last = loaded.trials[-1]
+        assert last['state'] == H.JOB_STATE_NEW and last._store is st
+        old = signal.signal(signal.SIGALRM, lambda *a: (_ for _ in ()).throw(TimeoutError()))
+        signal.alarm(30)
+        try:
+            H.fmin(lambda x: x ** 2, hp.uniform('x', -1, 1), algo=rand.suggest, max_evals=6,
+                   trials=loaded, rstate=np.random.RandomState(1))
+        finally:
+            signal.alarm(0)
+            signal.signal(signal.SIGALRM, old)
+        assert len(loaded) == 6
+        assert all(d['state'] == H.JOB_STATE_DONE for d in loaded.trials)
+        assert st.state.view().tolist() == [H.JOB_STATE_DONE] * 6
+    assert len(t) == 4 and t.trials[-1]['state'] == H.JOB_STATE_NEW   # original untouched
+
+
+def test_dropped_document_reassigned_enters_history():
+    """a tid dropped by a rebuild (its first loss NaN) whose
+    result is later reassigned to a finite loss enters the incrementally
+    synced history, as a fresh assembly (the reference's per-call rebuild)
+    includes it."""
+    dom = Domain(lambda x: 0, SPACE)
+    t = Trials()
+    hist = TrialHistory(dom)
+    plan = FakePlan(len(dom.space.labels), 64)
+    t.insert_trial_docs(rand.suggest([0, 1, 2], dom, t, 5))
+    t.refresh()
+    for i, d in enumerate(t.trials):
+        d['result'] = {'status': 'ok', 'loss': float('nan') if i == 1 else float(i)}
+        d['state'] = H.JOB_STATE_DONE
+    check(dom, t, hist, plan)
+    assert hist.tids == [0, 2]
+    t.insert_trial_docs(rand.suggest([3], dom, t, 6))
+    t.refresh()
+    t.trials[3]['result'] = {'status': 'ok', 'loss': 0.5}
+    t.trials[3]['state'] = H.JOB_STATE_DONE
+    t.trials[1]['result'] = {'status': 'ok', 'loss': 0.25}
+    check(dom, t, hist, plan)
+    assert hist.tids == [0, 1, 2, 3]
