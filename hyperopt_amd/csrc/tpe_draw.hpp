@@ -244,6 +244,59 @@ __device__ __attribute__((noinline)) inline double draw_one_ool(
   return draw_one(*Hp, *I, w, mu, sg, seed, gi, stream);
 }
 
+// Active-slot grids (ScoreArgs::compact).  Lane i of the wave tests slot
+// s0 + i (+ 64 per round) of the range [s0, s0 + n) for suggestion s; the
+// j-th active one (in slot order), or -1 when fewer are active.  Every lane
+// of the wave calls it (the result is wave-uniform).
+__device__ __forceinline__ int active_slot(const ScoreArgs &A, int s, int s0, int n, int j) {
+  const int lane = threadIdx.x & 63;
+  const Partial *res = A.results + (int64_t)s * A.n_hp;
+  int seen = 0;
+  for (int b = 0; b < n; b += 64) {
+    const int i = b + lane;
+    const bool act = i < n && hp_active(A.hps[A.level_hps[s0 + i]], res, A.cond_parent,
+                                        A.cond_branch);
+    uint64_t m = __ballot(act);
+    const int c = __popcll(m);
+    if (j < seen + c) {
+      for (int k = seen; k < j; ++k) m &= m - 1;
+      return s0 + b + __builtin_ctzll(m);
+    }
+    seen += c;
+  }
+  return -1;
+}
+// the same over the union of suggestions 0 .. n_sug - 1 (value lattices are
+// shared by every suggestion of a call)
+__device__ __forceinline__ int active_slot_any(const ScoreArgs &A, int n_sug, int s0, int n,
+                                               int j) {
+  const int lane = threadIdx.x & 63;
+  int seen = 0;
+  for (int b = 0; b < n; b += 64) {
+    const int i = b + lane;
+    bool act = false;
+    if (i < n) {
+      const tpe_hp &H = A.hps[A.level_hps[s0 + i]];
+      for (int s = 0; s < n_sug && !act; ++s)
+        act = hp_active(H, A.results + (int64_t)s * A.n_hp, A.cond_parent, A.cond_branch);
+    }
+    uint64_t m = __ballot(act);
+    const int c = __popcll(m);
+    if (j < seen + c) {
+      for (int k = seen; k < j; ++k) m &= m - 1;
+      return s0 + b + __builtin_ctzll(m);
+    }
+    seen += c;
+  }
+  return -1;
+}
+// the slot of draw / bucket grid row `row` of suggestion s over slots
+// [s0, s0 + n): the row itself, or with compact grids the row-th active slot
+// (-1: none; without compaction the caller still tests activity)
+__device__ __forceinline__ int row_slot(const ScoreArgs &A, int s, int s0, int n, int row) {
+  return A.compact ? active_slot(A, s, s0, n, row) : s0 + row;
+}
+
 // One draw block (k_draw<true>, or a draw row of the fused k_lattice): the
 // below mixture's table of (suggestion s, level slot) in LDS, then a
 // grid-stride pass over the chunk's candidates bx * blockDim + t (+ stride).
@@ -251,11 +304,14 @@ __device__ __attribute__((noinline)) inline double draw_one_ool(
 // 2048 draws.  K > CAP (a stale host routing decision) falls back to the
 // rejection sampler: the same distribution, never a silent NaN.
 template <int CAP>
-__device__ void draw_block(const ScoreArgs &A, int bx, int slot, int s, DrawTableT<CAP> &T,
+__device__ void draw_block(const ScoreArgs &A, int bx, int row, int s, DrawTableT<CAP> &T,
                            int64_t stride) {
+  const int slot = row_slot(A, s, 0, A.n_slots, row);
+  if (slot < 0) return;
   const int hp = A.level_hps[slot];
   const tpe_hp H = A.hps[hp];
-  if (!hp_active(H, A.results + (int64_t)s * A.n_hp, A.cond_parent, A.cond_branch)) return;
+  if (!A.compact && !hp_active(H, A.results + (int64_t)s * A.n_hp, A.cond_parent, A.cond_branch))
+    return;
   const int64_t sb = 2 * (int64_t)hp;
   const double *bw = A.mw + sb * A.kcap, *bmu = A.mmu + sb * A.kcap, *bsg = A.msig + sb * A.kcap;
   const int K = A.info[sb].K;

@@ -23,6 +23,8 @@
 using namespace tpe;
 
 static int lse_shift_min();
+static bool compact_on();
+static bool sort_by_rows();
 static bool wave_tiles_on();
 static bool small_sort_on();
 static int64_t chunk_budget();
@@ -420,7 +422,10 @@ int ensure_ext(tpe_engine *h, tpe_plan *p, size_t n) {
 // heaviest kind first (per-candidate erf, then log-sum-exp, then the lattice /
 // categorical lookups): the dispatcher hands out the long blocks first and the
 // short ones fill the CUs that finish early.
-int32_t set_score_groups(ScoreArgs &a, const int *kinds, int n_slots, int64_t cn) {
+// rows(b, e) (optional, compact grids): block rows for the slots [b, e) of a
+// group (active_bound), else one row per slot.
+template <typename Rows>
+int32_t set_score_groups(ScoreArgs &a, const int *kinds, int n_slots, int64_t cn, Rows rows) {
   a.n_groups = 0;
   int32_t blocks = 0, pstride = 1;
   auto weight = [](int kind) {
@@ -443,9 +448,10 @@ int32_t set_score_groups(ScoreArgs &a, const int *kinds, int n_slots, int64_t cn
       const int32_t nt = (int32_t)((std::max<int64_t>(cn, 0) + tc - 1) / tc);
       a.grp_kind[g] = kinds[j];
       a.grp_slot0[g] = j;
+      a.grp_slots[g] = k - j;
       a.grp_tiles[g] = nt;
       a.grp_block0[g] = blocks;
-      blocks += nt * (k - j);
+      blocks += nt * std::min<int32_t>(k - j, rows(j, k));
       pstride = std::max(pstride, nt);
       j = k;
     }
@@ -453,10 +459,49 @@ int32_t set_score_groups(ScoreArgs &a, const int *kinds, int n_slots, int64_t cn
   a.grp_block0[a.n_groups] = blocks;
   return pstride;
 }
+int32_t set_score_groups(ScoreArgs &a, const int *kinds, int n_slots, int64_t cn) {
+  return set_score_groups(a, kinds, n_slots, cn, [](int b, int e) { return e - b; });
+}
+
+// The most hps of hps[b, e) active together in one suggestion: the
+// unconditional ones, plus, for every condition parent, the most hps that
+// share one of its branch values.  (A parent takes one value per suggestion
+// and an active hp has a true condition: charge it to that condition's
+// parent; the hps charged to a parent share the branch it took.)
+int32_t active_bound(const tpe_plan *p, const int32_t *hps, int b, int e) {
+  int32_t n = 0;
+  std::vector<std::pair<int32_t, int32_t>> pb;  // (parent, branch) of every condition
+  for (int i = b; i < e; ++i) {
+    const tpe_hp &x = p->hps[hps[i]];
+    if (x.cond_count == 0) { ++n; continue; }
+    std::vector<std::pair<int32_t, int32_t>> mine;
+    for (int c = 0; c < x.cond_count; ++c)
+      mine.emplace_back(p->cond_parent[x.cond_begin + c], p->cond_branch[x.cond_begin + c]);
+    std::sort(mine.begin(), mine.end());
+    mine.erase(std::unique(mine.begin(), mine.end()), mine.end());
+    pb.insert(pb.end(), mine.begin(), mine.end());
+  }
+  std::sort(pb.begin(), pb.end());
+  for (size_t i = 0; i < pb.size();) {
+    int32_t best = 0;
+    size_t j = i;
+    while (j < pb.size() && pb[j].first == pb[i].first) {
+      size_t k = j;
+      while (k < pb.size() && pb[k] == pb[j]) ++k;
+      best = std::max<int32_t>(best, (int32_t)(k - j));
+      j = k;
+    }
+    n += best;
+    i = j;
+  }
+  return std::min<int32_t>(n, e - b);
+}
 
 void copy_groups(ScoreArgs &a, const ScoreArgs &g) {
   a.n_groups = g.n_groups;
+  a.compact = g.compact;
   for (int i = 0; i < kMaxGroups; ++i) {
+    a.grp_slots[i] = g.grp_slots[i];
     a.grp_kind[i] = g.grp_kind[i];
     a.grp_slot0[i] = g.grp_slot0[i];
     a.grp_tiles[i] = g.grp_tiles[i];
@@ -581,6 +626,16 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
   const bool lat_level = n_lat > 0 && p->lattice_on && rmax <= n_cand * n_sug &&
                          2 * ((p->kcap + 15) / 16) <= (int64_t)kLatChunks;
   if (!lat_level) n_lat = 0;
+  // conditional level: grids sized for the hps that can be active together
+  // (ScoreArgs::compact), not one row per hp -- the other branches of a
+  // choice cost no blocks
+  const int32_t *hl = p->levels[level].data();
+  const int32_t lvl_rows = active_bound(p, hl, 0, n_level);
+  const bool compact = compact_on() && lvl_rows < n_level;
+  const int32_t slot_rows = compact ? lvl_rows : n_level;
+  const int32_t lat_rows =
+      compact ? (int32_t)std::min<int64_t>(n_lat, n_sug * (int64_t)active_bound(p, hl, 0, n_lat))
+              : n_lat;
   const int64_t budget = chunk_budget();  // doubles
   int64_t chunk = std::max<int64_t>(
       1, std::min<int64_t>(std::max<int64_t>(n_cand, 1),
@@ -606,6 +661,10 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
     // beside the candidate draw (fork / join events; a parallel branch of the
     // captured graph), and the scoring launch waits for it
     ScoreArgs la = base_args(p, n_sug);
+    la.level_hps = lvl;
+    la.n_slots = n_level;
+    la.slot_rows = slot_rows;
+    la.compact = compact ? 1 : 0;
 #if TPE_LAT_SIDE
     hipStream_t sl = h->aux[0];
     CKH(hipEventRecord(p->ev_fork, st));
@@ -617,7 +676,7 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
     if (p->prof_cap > 0 && p->prof[1].n < p->prof_cap) pr = &p->prof[1];
     if (pr) CKH(hipEventRecord(pr->a[pr->n], sl));
     CKH(launch_lattice(la, p->levels[level].data(), p->hps.data(), p->lat.data(), n_lat,
-                       p->d_lat, sl));
+                       p->d_lat, sl, lat_rows));
     if (pr) {
       CKH(hipEventRecord(pr->b[pr->n], sl));
       pr->pairs[pr->n] = (double)level;
@@ -634,7 +693,13 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
   // one-row tiles double the count at the same per-pair arithmetic
   {
     int64_t lse_slots = 0;
-    for (int k : kinds) lse_slots += (k == KIND_LSE_G || k == KIND_LSE_L) ? 1 : 0;
+    for (int j = 0; j < n_level;) {  // active rows of the log-sum-exp runs
+      int k = j;
+      while (k < n_level && kinds[k] == kinds[j]) ++k;
+      if (kinds[j] == KIND_LSE_G || kinds[j] == KIND_LSE_L)
+        lse_slots += compact ? active_bound(p, hl, j, k) : k - j;
+      j = k;
+    }
     const int64_t blocks2 = n_sug * lse_slots * ((n_cand + 127) / 128);
     if (lse_slots > 0 && blocks2 < 3 * kNumCUs)
       for (int &k : kinds)
@@ -648,7 +713,7 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
     // tiles then skip the component blocks that are exact zeros for them,
     // on wave tiles when the wave-wide exponent is on (prune mode 2)
     const bool sorted_draw = !fuse_draw && table_draw &&
-                             cn * n_sug * n_level >= ((int64_t)1 << 22);
+                             cn * n_sug * (sort_by_rows() ? slot_rows : n_level) >= ((int64_t)1 << 22);
     // small draws of >= kSmallSortMin candidates: the log-sum-exp slots are
     // value-bucketed too (k_bucket, stable, <= 8192 per bucketing chunk) and
     // pruned on the 8-wave tiles
@@ -668,7 +733,10 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
       for (int &k : ck)
         k = k == KIND_LSE_G ? KIND_LSE_G1 : k == KIND_LSE_L ? KIND_LSE_L1 : k;
     ScoreArgs grid{};
-    const int32_t pstride = set_score_groups(grid, ck.data(), n_level, cn);
+    grid.compact = compact ? 1 : 0;
+    const int32_t pstride = set_score_groups(grid, ck.data(), n_level, cn, [&](int b, int e) {
+      return compact ? active_bound(p, hl, b, e) : e - b;
+    });
     if (pstride < 0) return fail(h, TPE_E_INVALID, "level slots not grouped by lpdf kind");
     int rc = ensure_suggest_state(h, p, n_sug, (size_t)n_sug * p->P * pstride);
     if (rc) return rc;
@@ -685,6 +753,7 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
     a.accumulate = c0 > 0 ? 1 : 0;
     a.level_hps = lvl;
     a.n_slots = n_level;
+    a.slot_rows = slot_rows;
     a.cand_slot0 = 0;
     for (int i = 0; i < kInlineSeeds && i < n_sug; ++i) a.seed_inline[i] = p->h_seeds[i];
     a.n_inline_seeds = (int32_t)std::min<int64_t>(n_sug, kInlineSeeds);
@@ -696,7 +765,7 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
       if (p->prof_cap > 0 && p->prof[1].n < p->prof_cap) pr = &p->prof[1];
       if (pr) CKH(hipEventRecord(pr->a[pr->n], st));
       CKH(launch_lattice_draw(a, p->levels[level].data(), p->hps.data(), p->lat.data(), n_lat,
-                              p->d_lat, st));
+                              p->d_lat, st, lat_rows));
       if (pr) {
         CKH(hipEventRecord(pr->b[pr->n], st));
         pr->pairs[pr->n] = (double)level;
@@ -747,6 +816,7 @@ int run_external(tpe_engine *h, tpe_plan *p, int32_t hp, const double *ext, int6
   a.pstride = pstride;
   a.level_hps = p->d_all_hps + hp;
   a.n_slots = 1;
+  a.slot_rows = 1;
   a.out_lb = lb;
   a.out_la = la;
   a.force_active = 1;
@@ -1577,6 +1647,25 @@ static bool wave_tiles_on() {
 // (TPE_SMALL_SORT=1).  Measured at config 2 (4096 candidates): the skip drops
 // 80 % of the pairs and k_score from 33 to 23 us, but the extra k_bucket
 // launch costs more than that (suggest 70 -> 78 us)
+// compact (active-slot) grids of conditional levels; TPE_COMPACT=0 turns
+// them off (A/B measurements)
+static bool compact_on() {
+  static const bool on = [] {
+    const char *e = std::getenv("TPE_COMPACT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+// the large-draw (value-bucketed) path is picked by the draws of the hps
+// that can be active (TPE_SORT_ROWS=1) instead of every hp of the level
+static bool sort_by_rows() {
+  static const bool on = [] {
+    const char *e = std::getenv("TPE_SORT_ROWS");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 static bool small_sort_on() {
   static const bool v = [] {
     const char *e = std::getenv("TPE_SMALL_SORT");

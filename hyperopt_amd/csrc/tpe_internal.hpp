@@ -170,6 +170,14 @@ struct ScoreArgs {
   int32_t grp_slot0[kMaxGroups];
   int32_t grp_tiles[kMaxGroups];       // tiles per slot of the group
   int32_t grp_block0[kMaxGroups + 1];  // first block of each group; [n_groups] = total
+  int32_t grp_slots[kMaxGroups];       // slots of each group
+  // active-slot grids (conditional levels): a launch has rows for at most
+  // slot_rows slots per suggestion (the most its hps can have active
+  // together, active_bound) instead of one per slot; row j takes the j-th
+  // active slot (active_slot), so the inactive branches of a choice cost no
+  // blocks.  compact = 0: row j is slot j (every slot has its rows).
+  int32_t compact;
+  int32_t slot_rows;                   // draw / bucket grids: rows over the level's slots
   int32_t force_active;      // ignore conditions (operator-level scoring)
   int32_t accumulate;        // merge with results of an earlier candidate chunk
   unsigned long long *census;  // optional [kCensus] pair counters (tpe_plan_census)
@@ -233,17 +241,24 @@ struct LatJobs {
   int32_t n_jobs;
   int32_t draw_gx;
   int32_t draw_blocks;
-  int32_t pad;
+  // compact: grid row y < n_jobs is the y-th of the level's first n_lat
+  // (lattice) slots active in some suggestion, its descriptor read from
+  // A.hps / A.lat_info (job[] unused); one launch for every lattice hp
+  int32_t compact;
+  int32_t n_lat;
+  int32_t pad[3];
 };
 constexpr int kFuseTab = 32;  // below K of a draw fused into k_lattice (LDS table)
+// lat_rows in (0, n_lat): compact rows (LatJobs::compact), one launch
 hipError_t launch_lattice(const ScoreArgs &a, const int32_t *hps_of_level, const tpe_hp *hps,
-                          const LatInfo *lat, int32_t n_lat, double2 *lat_out, hipStream_t st);
+                          const LatInfo *lat, int32_t n_lat, double2 *lat_out, hipStream_t st,
+                          int32_t lat_rows);
 // the same lattice launch with the level's candidate draw (draw args `a`, one
 // candidate per thread, every below K <= kFuseTab) in extra blocks of it: the
 // two only need the fitted mixtures and run side by side
 hipError_t launch_lattice_draw(const ScoreArgs &a, const int32_t *hps_of_level, const tpe_hp *hps,
                                const LatInfo *lat, int32_t n_lat, double2 *lat_out,
-                               hipStream_t st);
+                               hipStream_t st, int32_t lat_rows);
 constexpr int kTabCap = 2048;  // below-mixture components of the LDS draw table
 hipError_t launch_draw(const ScoreArgs &a, bool table, hipStream_t st);
 // large draws: each block draws kSortedBlock consecutive candidates of a slot

@@ -109,10 +109,13 @@ __global__ __launch_bounds__(kDrawThreads) void k_draw(ScoreArgs A) {
     __shared__ DrawTable T;
     draw_block<kTabCap>(A, blockIdx.x, blockIdx.y, blockIdx.z, T, (int64_t)gridDim.x * blockDim.x);
   } else {
-    const int slot = blockIdx.y, s = blockIdx.z;
+    const int s = blockIdx.z;
+    const int slot = row_slot(A, s, 0, A.n_slots, blockIdx.y);
+    if (slot < 0) return;
     const int hp = A.level_hps[slot];
     const tpe_hp H = A.hps[hp];
-    if (!hp_active(H, A.results + (int64_t)s * A.n_hp, A.cond_parent, A.cond_branch)) return;
+    if (!A.compact && !hp_active(H, A.results + (int64_t)s * A.n_hp, A.cond_parent, A.cond_branch))
+      return;
     const int64_t sb = 2 * (int64_t)hp;
     const double *bw = A.mw + sb * A.kcap, *bmu = A.mmu + sb * A.kcap, *bsg = A.msig + sb * A.kcap;
     const uint64_t seed = suggestion_seed(A, s);
@@ -137,15 +140,11 @@ __global__ __launch_bounds__(kDrawThreads) void k_draw(ScoreArgs A) {
 // and the argmax tie-break uses the original index.
 constexpr int kSortBuckets = 256;
 
-// the scoring kind of a level slot: the groups are emitted heaviest kind
-// first (set_score_groups), not in slot order, so each group's slot range is
-// recovered from its block count
+// the scoring kind of a level slot (the groups are emitted heaviest kind
+// first, set_score_groups, not in slot order)
 __device__ __forceinline__ int slot_kind(const ScoreArgs &A, int slot) {
-  for (int g = 0; g < A.n_groups; ++g) {
-    const int nt = A.grp_tiles[g];
-    const int ns = nt > 0 ? (A.grp_block0[g + 1] - A.grp_block0[g]) / nt : 0;
-    if (slot >= A.grp_slot0[g] && slot < A.grp_slot0[g] + ns) return A.grp_kind[g];
-  }
+  for (int g = 0; g < A.n_groups; ++g)
+    if (slot >= A.grp_slot0[g] && slot < A.grp_slot0[g] + A.grp_slots[g]) return A.grp_kind[g];
   return -1;
 }
 
@@ -164,10 +163,13 @@ template <int CAP, bool EXT>
 __device__ __forceinline__ void sorted_block(const ScoreArgs &A, int32_t *__restrict__ pos_out,
                                              const double *__restrict__ src,
                                              SortedDrawLds<CAP> &L) {
-  const int slot = blockIdx.y, s = blockIdx.z;
+  const int s = blockIdx.z;
+  const int slot = row_slot(A, s, 0, A.n_slots, blockIdx.y);
+  if (slot < 0) return;
   const int hp = A.level_hps[slot];
   const tpe_hp H = A.hps[hp];
-  if (!A.force_active && !hp_active(H, A.results + (int64_t)s * A.n_hp, A.cond_parent, A.cond_branch))
+  if (!A.force_active && !A.compact &&
+      !hp_active(H, A.results + (int64_t)s * A.n_hp, A.cond_parent, A.cond_branch))
     return;
   const int64_t sb = 2 * (int64_t)hp;
   const double *bw = A.mw + sb * A.kcap, *bmu = A.mmu + sb * A.kcap, *bsg = A.msig + sb * A.kcap;
@@ -259,14 +261,17 @@ __global__ __launch_bounds__(1024) void k_bucket(ScoreArgs A, int32_t slot_begin
   extern __shared__ __attribute__((aligned(16))) double dyn_lds[];
   __shared__ int cnt[16 * kBuckets];
   __shared__ double red_lo[16], red_hi[16];
-  const int slot = slot_begin + (int)blockIdx.y, s = blockIdx.z;
+  const int s = blockIdx.z;
+  const int slot = row_slot(A, s, slot_begin, A.n_slots - slot_begin, blockIdx.y);
+  if (slot < 0) return;
   const int hp = A.level_hps[slot];
   const tpe_hp H = A.hps[hp];
   const int kind = score_kind(H);
   // erf kinds always; log-sum-exp kinds when the launch prunes them (lse_pos)
   const bool lse = kind == KIND_LSE_G || kind == KIND_LSE_L;
   if (!(kind == KIND_ERF_G || kind == KIND_ERF_L || (lse && A.lse_pos))) return;
-  if (!hp_active(H, A.results + (int64_t)s * A.n_hp, A.cond_parent, A.cond_branch)) return;
+  if (!A.compact && !hp_active(H, A.results + (int64_t)s * A.n_hp, A.cond_parent, A.cond_branch))
+    return;
   const int64_t base = (int64_t)blockIdx.x * kSortMax;
   if (base >= A.n_cand) return;
   const int n = (int)min<int64_t>(kSortMax, A.n_cand - base);
@@ -599,10 +604,11 @@ hipError_t launch_draw(const ScoreArgs &a, bool table, hipStream_t st) {
   if (a.n_slots <= 0 || a.n_suggest <= 0 || a.n_cand <= 0) return hipSuccess;
   // one candidate per thread while that leaves the grid short (latency), up
   // to 8 per thread for large chunks (the per-block table build amortised)
-  const int64_t per = a.n_cand * a.n_slots * a.n_suggest >= ((int64_t)1 << 22) ? 8 : 1;
+  const int64_t per = a.n_cand * a.slot_rows * a.n_suggest >= ((int64_t)1 << 22) ? 8 : 1;
   const unsigned gx = (unsigned)((a.n_cand + kDrawThreads * per - 1) / (kDrawThreads * per));
-  if (table) k_draw<true><<<dim3(gx, a.n_slots, a.n_suggest), kDrawThreads, 0, st>>>(a);
-  else k_draw<false><<<dim3(gx, a.n_slots, a.n_suggest), kDrawThreads, 0, st>>>(a);
+  const dim3 g(gx, (unsigned)a.slot_rows, a.n_suggest);
+  if (table) k_draw<true><<<g, kDrawThreads, 0, st>>>(a);
+  else k_draw<false><<<g, kDrawThreads, 0, st>>>(a);
   return hipGetLastError();
 }
 
@@ -610,7 +616,7 @@ hipError_t launch_draw_sorted(const ScoreArgs &a, bool small_table, int32_t *pos
                               hipStream_t st) {
   if (a.n_slots <= 0 || a.n_suggest <= 0 || a.n_cand <= 0) return hipSuccess;
   const unsigned gx = (unsigned)((a.n_cand + kSortedBlock - 1) / kSortedBlock);
-  const dim3 g(gx, a.n_slots, a.n_suggest);
+  const dim3 g(gx, (unsigned)a.slot_rows, a.n_suggest);
   if (small_table) k_draw_sorted<kFuseTab><<<g, kDrawThreads, 0, st>>>(a, pos_out);
   else k_draw_sorted<kTabCap><<<g, kDrawThreads, 0, st>>>(a, pos_out);
   return hipGetLastError();
@@ -627,7 +633,8 @@ hipError_t launch_sort_ext(const ScoreArgs &a, const double *src, int32_t *pos_o
 hipError_t launch_bucket(const ScoreArgs &a, int32_t slot_begin, int32_t *pos_out, hipStream_t st) {
   if (a.n_slots <= slot_begin || a.n_suggest <= 0 || a.n_cand <= 0) return hipSuccess;
   const unsigned gx = (unsigned)((a.n_cand + kSortMax - 1) / kSortMax);
-  k_bucket<<<dim3(gx, a.n_slots - slot_begin, a.n_suggest), 1024, (size_t)kSortMax * 9, st>>>(
+  const unsigned rows = (unsigned)std::min(a.n_slots - slot_begin, a.slot_rows);
+  k_bucket<<<dim3(gx, rows, a.n_suggest), 1024, (size_t)kSortMax * 9, st>>>(
       a, slot_begin, pos_out);
   return hipGetLastError();
 }

@@ -616,7 +616,7 @@ struct ScoreSmem {
 
 template <int KIND, bool CENSUS>
 __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, int slot, int tile,
-                                           int ntiles) {
+                                           int ntiles, bool known_active) {
   constexpr int KR = tile_rows(KIND);
   constexpr bool LSE = kind_lse(KIND);
   constexpr bool WT = tile_waves(KIND) > 1;  // wave tiles: own candidates, all components
@@ -628,8 +628,8 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
   const tpe_hp H = A.hps[hp];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   SSTAMP(0);
-  const bool act = A.force_active || hp_active(H, A.results + (int64_t)s * A.n_hp,
-                                                  A.cond_parent, A.cond_branch);
+  const bool act = A.force_active || known_active ||
+                   hp_active(H, A.results + (int64_t)s * A.n_hp, A.cond_parent, A.cond_branch);
   if (!act) {  // one record says "inactive"; no tickets are taken
     if (tile == 0 && threadIdx.x == 0)
       A.results[(int64_t)s * A.n_hp + hp] = Partial{NAN, NAN, -1, 0, 0};
@@ -934,6 +934,19 @@ __device__ __forceinline__ int xcd_local(int l, int n, int p) {
   return off + ((l - fq) >> 3);
 }
 
+// Compact grids: the group's rows are its active slots in slot order; the
+// first row's first tile also writes the "inactive" record of every slot of
+// the group that has no rows (the record score_tile writes for an inactive
+// slot of a full grid).
+__device__ __forceinline__ void mark_inactive(const ScoreArgs &A, int s, int s0, int n) {
+  if (threadIdx.x >= 64) return;
+  Partial *res = A.results + (int64_t)s * A.n_hp;
+  for (int i = (int)threadIdx.x; i < n; i += 64) {
+    const int hp = A.level_hps[s0 + i];
+    if (!hp_active(A.hps[hp], res, A.cond_parent, A.cond_branch)) res[hp] = Partial{NAN, NAN, -1, 0, 0};
+  }
+}
+
 template <bool ERFK, bool CENSUS>
 __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(6)))
 void k_score(ScoreArgs A) {
@@ -944,18 +957,26 @@ void k_score(ScoreArgs A) {
   const int nt = A.grp_tiles[g];
   const int local = xcd_local(b - A.grp_block0[g], A.grp_block0[g + 1] - A.grp_block0[g],
                               (int)(((int64_t)blockIdx.y * gridDim.x + A.grp_block0[g]) & 7));
-  const int slot = A.grp_slot0[g] + local / nt, tile = local % nt;
+  int slot = A.grp_slot0[g] + local / nt;
+  const int tile = local % nt;
+  if (A.compact) {
+    const int row = local / nt;
+    if (row == 0 && tile == 0) mark_inactive(A, blockIdx.y, A.grp_slot0[g], A.grp_slots[g]);
+    slot = active_slot(A, blockIdx.y, A.grp_slot0[g], A.grp_slots[g], row);
+    if (slot < 0) return;
+  }
+  const bool known = A.compact != 0;
   switch (A.grp_kind[g]) {
-    case KIND_LSE_G: score_tile<KIND_LSE_G, CENSUS>(A, sm, slot, tile, nt); break;
-    case KIND_LSE_L: score_tile<KIND_LSE_L, CENSUS>(A, sm, slot, tile, nt); break;
-    case KIND_LSE_G1: score_tile<KIND_LSE_G1, CENSUS>(A, sm, slot, tile, nt); break;
-    case KIND_LSE_L1: score_tile<KIND_LSE_L1, CENSUS>(A, sm, slot, tile, nt); break;
-    case KIND_LSE_GW: score_tile<KIND_LSE_GW, CENSUS>(A, sm, slot, tile, nt); break;
-    case KIND_LSE_LW: score_tile<KIND_LSE_LW, CENSUS>(A, sm, slot, tile, nt); break;
-    case KIND_ERF_G: if constexpr (ERFK) score_tile<KIND_ERF_G, CENSUS>(A, sm, slot, tile, nt); break;
-    case KIND_ERF_L: if constexpr (ERFK) score_tile<KIND_ERF_L, CENSUS>(A, sm, slot, tile, nt); break;
-    case KIND_LAT: score_tile<KIND_LAT, CENSUS>(A, sm, slot, tile, nt); break;
-    default: score_tile<KIND_CAT, CENSUS>(A, sm, slot, tile, nt); break;
+    case KIND_LSE_G: score_tile<KIND_LSE_G, CENSUS>(A, sm, slot, tile, nt, known); break;
+    case KIND_LSE_L: score_tile<KIND_LSE_L, CENSUS>(A, sm, slot, tile, nt, known); break;
+    case KIND_LSE_G1: score_tile<KIND_LSE_G1, CENSUS>(A, sm, slot, tile, nt, known); break;
+    case KIND_LSE_L1: score_tile<KIND_LSE_L1, CENSUS>(A, sm, slot, tile, nt, known); break;
+    case KIND_LSE_GW: score_tile<KIND_LSE_GW, CENSUS>(A, sm, slot, tile, nt, known); break;
+    case KIND_LSE_LW: score_tile<KIND_LSE_LW, CENSUS>(A, sm, slot, tile, nt, known); break;
+    case KIND_ERF_G: if constexpr (ERFK) score_tile<KIND_ERF_G, CENSUS>(A, sm, slot, tile, nt, known); break;
+    case KIND_ERF_L: if constexpr (ERFK) score_tile<KIND_ERF_L, CENSUS>(A, sm, slot, tile, nt, known); break;
+    case KIND_LAT: score_tile<KIND_LAT, CENSUS>(A, sm, slot, tile, nt, known); break;
+    default: score_tile<KIND_CAT, CENSUS>(A, sm, slot, tile, nt, known); break;
   }
 }
 
@@ -1063,24 +1084,50 @@ __global__ __launch_bounds__(kLatThreads) void k_lattice(ScoreArgs A, LatJobs J,
     if ((int)blockIdx.y >= J.n_jobs) {
       const int d = ((int)blockIdx.y - J.n_jobs) * (int)gridDim.x + (int)blockIdx.x;
       if (d >= J.draw_blocks) return;
-      const int per_s = J.draw_gx * A.n_slots;
+      const int per_s = J.draw_gx * A.slot_rows;
       draw_block<kFuseTab>(A, d % J.draw_gx, (d % per_s) / J.draw_gx, d / per_s,
                            *reinterpret_cast<DrawTableT<kFuseTab> *>(csum),
                            (int64_t)J.draw_gx * blockDim.x);
       return;
     }
   }
-  const LatJob &jb = J.job[blockIdx.y];
   const int64_t pt = blockIdx.x;
+  if (J.compact) {
+    const int slot = active_slot_any(A, A.n_suggest, 0, J.n_lat, blockIdx.y);
+    if (slot < 0) return;
+    const int hp = A.level_hps[slot];
+    const LatInfo L = A.lat_info[hp];
+    if (pt >= L.R) return;
+    const tpe_hp H = A.hps[hp];
+    if (H.family == TPE_LGMM) lattice_point<true>(A, H, hp, L, pt, csum, out);
+    else lattice_point<false>(A, H, hp, L, pt, csum, out);
+    return;
+  }
+  const LatJob &jb = J.job[blockIdx.y];
   if (pt >= jb.L.R) return;
   if (jb.H.family == TPE_LGMM) lattice_point<true>(A, jb.H, jb.hp, jb.L, pt, csum, out);
   else lattice_point<false>(A, jb.H, jb.hp, jb.L, pt, csum, out);
 }
 
 hipError_t launch_lattice(const ScoreArgs &a, const int32_t *hps_of_level, const tpe_hp *hps,
-                          const LatInfo *lat, int32_t n_lat, double2 *lat_out, hipStream_t st) {
+                          const LatInfo *lat, int32_t n_lat, double2 *lat_out, hipStream_t st,
+                          int32_t lat_rows) {
   const int64_t nch = 2 * ((a.kcap + kChunk - 1) / kChunk);
   if (nch > kLatChunks) return hipErrorInvalidValue;
+  if (lat_rows > 0 && lat_rows < n_lat) {
+    // compact: one launch, rows = the most lattice hps active in some suggestion
+    LatJobs J{};
+    int64_t rmax = 0;
+    for (int32_t i = 0; i < n_lat; ++i) rmax = std::max<int64_t>(rmax, lat[hps_of_level[i]].R);
+    if (rmax > kLatMaxR) return hipErrorInvalidValue;
+    if (rmax <= 0) return hipSuccess;
+    J.n_jobs = lat_rows;
+    J.compact = 1;
+    J.n_lat = n_lat;
+    k_lattice<false><<<dim3((unsigned)rmax, (unsigned)lat_rows), kLatThreads,
+                       (size_t)nch * sizeof(double), st>>>(a, J, lat_out);
+    return hipGetLastError();
+  }
   for (int32_t i0 = 0; i0 < n_lat; i0 += kLatJobs) {
     LatJobs J{};
     int64_t rmax = 0;
@@ -1107,7 +1154,7 @@ const void *lattice_draw_kernel_fn() { return reinterpret_cast<const void *>(&k_
 
 hipError_t launch_lattice_draw(const ScoreArgs &a, const int32_t *hps_of_level, const tpe_hp *hps,
                                const LatInfo *lat, int32_t n_lat, double2 *lat_out,
-                               hipStream_t st) {
+                               hipStream_t st, int32_t lat_rows) {
   static_assert(kLatThreads == 256, "draw rows run k_draw's 256-thread blocks");
   const int64_t nch = 2 * ((a.kcap + kChunk - 1) / kChunk);
   if (nch > kLatChunks || n_lat < 1 || n_lat > kLatJobs || a.n_cand <= 0) return hipErrorInvalidValue;
@@ -1122,14 +1169,19 @@ hipError_t launch_lattice_draw(const ScoreArgs &a, const int32_t *hps_of_level, 
   }
   if (rmax > kLatMaxR || rmax <= 0) return hipErrorInvalidValue;
   const int64_t gx = (a.n_cand + kLatThreads - 1) / kLatThreads;
-  const int64_t draws = gx * a.n_slots * a.n_suggest;
+  const int64_t draws = gx * a.slot_rows * a.n_suggest;
   if (draws > ((int64_t)1 << 30)) return hipErrorInvalidValue;
   J.n_jobs = n_lat;
+  if (lat_rows > 0 && lat_rows < n_lat) {  // compact lattice rows (launch_lattice)
+    J.n_jobs = lat_rows;
+    J.compact = 1;
+    J.n_lat = n_lat;
+  }
   J.draw_gx = (int32_t)gx;
   J.draw_blocks = (int32_t)draws;
   const int64_t rows = (draws + rmax - 1) / rmax;
   const size_t lds = std::max<size_t>((size_t)nch * sizeof(double), sizeof(DrawTableT<kFuseTab>));
-  k_lattice<true><<<dim3((unsigned)rmax, (unsigned)(n_lat + rows)), kLatThreads, lds, st>>>(
+  k_lattice<true><<<dim3((unsigned)rmax, (unsigned)(J.n_jobs + rows)), kLatThreads, lds, st>>>(
       a, J, lat_out);
   return hipGetLastError();
 }
