@@ -316,6 +316,8 @@ def main():
     ap.add_argument('--n-cand', type=int, default=0,
                     help='override candidates per suggest (secondary measurements only)')
     ap.add_argument('--cpu-seconds', type=float, default=10.0)
+    ap.add_argument('--prune', type=int, default=3, choices=[0, 1, 2, 3],
+                    help='log-sum-exp prune mode of large draws (tpe_plan_set_prune; A/B)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-e2e', action='store_true')
     ap.add_argument('--parallelism', default='auto', choices=['auto', 'single', 'sharded'],
@@ -363,6 +365,7 @@ def main():
     dom, losses, vals, active = build_workload(args.config)
     hps, conds, pprior = dom.space.engine_tables()
     plan = E.Plan(eng, hps, conds, pprior, max_trials=losses.size)
+    plan.set_prune(args.prune)
     # history resident in HBM before the timed region
     d_losses = torch.from_numpy(np.ascontiguousarray(losses)).cuda()
     d_vals = torch.from_numpy(np.ascontiguousarray(vals)).cuda()
@@ -475,7 +478,9 @@ def report(args, C, eng, world, mode, elapsed, value, pairs_step, pairs_suggest,
     # quantized pairs (the per-wave exact-zero skips cost no erf).  LSE pairs
     # are priced at the faster of the two pair sequences k_score has (per
     # group max + lift, or one exponent per wave), whichever each wave ran
-    lse_peak_exact, lse_peak_shift = eng.microbench(3), eng.microbench(5)
+    # (one-exponent pairs: fp64 quadratic in prune mode 2, block-local fp32 in 3)
+    lse_peak_exact = eng.microbench(3)
+    lse_peak_shift = eng.microbench(6 if args.prune == 3 else 5)
     lse_peak = max(lse_peak_exact, lse_peak_shift)
     erf_peak = eng.microbench(4)
     lse_pairs = kinds.get('lse_gmm', 0.0) + kinds.get('lse_lgmm', 0.0)
@@ -509,7 +514,9 @@ def report(args, C, eng, world, mode, elapsed, value, pairs_step, pairs_suggest,
                      'quantized erf pairs) / launch time; achieved = frac x peak, in pairs/s of '
                      'the fastest (one-exponent) LSE form; peaks are microkernels of exactly the '
                      'pair arithmetic (LSE pair: 2 fp64 FMA + cvt + v_exp_f32 + fp32/fp64 sum, '
-                     'SURVEY 8d "1 exp + 6 flops"; quantized pair: 2 OCML fp64 erf + 8 flops)',
+                     'SURVEY 8d "1 exp + 6 flops"; prune mode 3 one-exponent pair: 1 packed '
+                     'fp32 FMA pair per 2 components + v_exp_f32 + sums; quantized pair: 2 OCML '
+                     'fp64 erf + 8 flops)',
                 lse_evaluated_shifted_pairs_per_launch=lse_shift,
                 lse_pairs_per_launch=lse_pairs, lse_evaluated_pairs_per_launch=lse_exec,
                 erf_pairs_per_launch=kinds.get('erf_gmm', 0.0) + kinds.get('erf_lgmm', 0.0),
@@ -538,8 +545,11 @@ def report(args, C, eng, world, mode, elapsed, value, pairs_step, pairs_suggest,
         'higher_is_better': True,
         'scaling': 'weak' if mode == 'replicas' else 'strong',
         'vs_baseline': None,
-        'dtype': 'f64 (log-sum-exp: fp64 exponent and accumulation, fp32 exp2 of the '
-                 'shifted term; quantized: fp64 erf)',
+        'dtype': ('f64 (log-sum-exp: fp64 accumulation, fp32 exp2 of the shifted term, '
+                  'its argument from an fp32 block-local quadratic (mode 3); quantized: fp64 erf)'
+                  if args.prune == 3 else
+                  'f64 (log-sum-exp: fp64 exponent and accumulation, fp32 exp2 of the '
+                  'shifted term; quantized: fp64 erf)'),
         'data': 'synthetic (SURVEY 8(d) histories: RandomState seeds as in tests/big_configs.py)',
         'config': {
             'workload': C['desc'],

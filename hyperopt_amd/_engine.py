@@ -519,9 +519,9 @@ class Plan(object):
 
     def set_prune(self, mode):
         """Log-sum-exp on bucketed large draws (tpe_plan_set_prune): 0 / False
-        every pair, 1 skip negligible component blocks, 2 / True (default)
-        skip + one exponent per wave."""
-        mode = 2 if mode is True else int(mode)
+        every pair, 1 skip negligible component blocks, 2 skip + one exponent
+        per wave, 3 / True (default) the same with block-local fp32 pairs."""
+        mode = 3 if mode is True else int(mode)
         e = self.engine
         with e.lock:
             e.check(e.lib.tpe_plan_set_prune(self.p, mode))

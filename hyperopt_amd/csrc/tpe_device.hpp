@@ -191,7 +191,8 @@ __device__ __forceinline__ Coef make_coef(const tpe_hp &H, double w, double mu, 
 // must be active), written by the group's first lane into the block's w-row
 // as 4 floats rounded outward (tpe_internal.hpp, kLseDeadBase).  NaN terms
 // disable the skip of the block.
-__device__ __forceinline__ void store_lse_envelope(Coef *table, int64_t k, EnvTerm e, bool valid) {
+__device__ __forceinline__ void store_lse_envelope(Coef *table, int64_t k, EnvTerm e, bool valid,
+                                                   const Coef &cf, Coef32 *t32) {
   // padding lanes (valid = false) contribute the neutral element
   double lo = valid ? e.m : INFINITY, hi = valid ? e.m : -INFINITY;
   double cm = !valid ? -INFINITY : (e.c == e.c) ? e.c : INFINITY, am = valid ? e.a2 : INFINITY;
@@ -206,6 +207,28 @@ __device__ __forceinline__ void store_lse_envelope(Coef *table, int64_t k, EnvTe
   lo = fmin(lo, dppd<kDppHalfMirror>(lo)); hi = fmax(hi, dppd<kDppHalfMirror>(hi));
   cm = fmax(cm, dppd<kDppHalfMirror>(cm)); am = fmin(am, dppd<kDppHalfMirror>(am));
   bad |= dpp<kDppHalfMirror>((int)bad) != 0;
+  // block-local fp32 form (Coef32): expand the quadratic about the block's
+  // mu' midpoint in fp64, alpha relative to an integer block base
+  {
+    const double cen = (lo <= hi) ? 0.5 * (lo + hi) : 0.0;
+    const double al = valid ? cf.x + cen * (cf.y + cen * cf.z) : -INFINITY;
+    const double be = valid ? cf.y + 2.0 * cen * cf.z : 0.0;
+    double amax = (al == al) ? al : -INFINITY;
+    amax = fmax(amax, dppd<kDppXor1>(amax));
+    amax = fmax(amax, dppd<kDppXor2>(amax));
+    amax = fmax(amax, dppd<kDppHalfMirror>(amax));
+    const double base = (amax > -1.0e300 && amax < 1.0e300) ? floor(amax) : 0.0;
+    Coef32 *b = t32 + k / kCoefBlock;
+    const int j = (int)(k % kCoefBlock);
+    b->a[j] = (float)(al - base);
+    b->b[j] = (float)be;
+    b->c[j] = valid ? (float)cf.z : 0.0f;
+    if (j == 0) {
+      b->center = cen;
+      b->base = (float)base;
+      b->pad0 = 0.0f;
+    }
+  }
   if (k % kCoefBlock) return;
   float *out = reinterpret_cast<float *>(reinterpret_cast<double *>(table) + coef_off(k, 3));
   const float flo = (float)lo, fhi = (float)hi, fc = (float)cm, fa = (float)am;

@@ -63,6 +63,7 @@ struct tpe_plan {
   int64_t scap = 0;
   MixInfo *d_info = nullptr;
   Coef *d_coef = nullptr;
+  Coef32 *d_coef32 = nullptr;  // [2P][kcap / kCoefBlock] block-local fp32 LSE terms
   int64_t n = 0;  // history length
   // suggestion state
   int64_t s_cap = 0;
@@ -80,8 +81,9 @@ struct tpe_plan {
   LatInfo *d_lat_info = nullptr;
   double2 *d_lat = nullptr;
   bool lattice_on = true;
-  int32_t prune_mode = 2;  // log-sum-exp on bucketed tiles (tpe_plan_set_prune): 0 full,
-                           // 1 block skip, 2 block skip + one exponent per wave
+  int32_t prune_mode = 3;  // log-sum-exp on bucketed tiles (tpe_plan_set_prune): 0 full,
+                           // 1 block skip, 2 block skip + one exponent per wave,
+                           // 3 the same with block-local fp32 pairs
   hipEvent_t ev_fork = nullptr, ev_join[8] = {};
   double *d_ext = nullptr, *d_lb = nullptr, *d_la = nullptr;
   size_t ext_cap = 0;
@@ -177,7 +179,7 @@ void plan_free_buffers(tpe_plan *p) {
                   p->d_losses, p->d_vals, p->d_active, p->d_below, p->d_mw, p->d_mmu,
                   p->d_msig, p->d_scratch, p->d_info, p->d_coef, p->d_results, p->d_seeds,
                   p->d_partial, p->d_ext, p->d_lb, p->d_la, p->d_cand, p->d_cpos,
-                  p->d_ticket, p->d_sortbuf, p->d_census, p->d_lat_info, p->d_lat};
+                  p->d_ticket, p->d_sortbuf, p->d_census, p->d_lat_info, p->d_lat, p->d_coef32};
   for (void *b : bufs) dfree(b);
   if (p->ev0) (void)hipEventDestroy(p->ev0);
   if (p->ev1) (void)hipEventDestroy(p->ev1);
@@ -351,6 +353,7 @@ int plan_build(tpe_engine *h, const tpe_space *sp, int64_t max_trials, tpe_plan 
   CKH(dalloc(&p->d_census, kCensus));
   CKH(hipMemset(p->d_census, 0, kCensus * sizeof(unsigned long long)));
   CKH(dalloc(&p->d_coef, (size_t)slots * kcap));
+  CKH(dalloc(&p->d_coef32, (size_t)slots * (kcap / kCoefBlock)));
   CKH(hipEventCreate(&p->ev0));
   CKH(hipEventCreate(&p->ev1));
   CKH(hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming));
@@ -537,6 +540,7 @@ ScoreArgs base_args(tpe_plan *p, int64_t n_sug) {
   a.cond_branch = p->d_cb;
   a.info = p->d_info;
   a.coef = p->d_coef;
+  a.coef32 = p->d_coef32;
   a.mw = p->d_mw;
   a.mmu = p->d_mmu;
   a.msig = p->d_msig;
@@ -570,6 +574,7 @@ FitArgs fit_args(tpe_plan *p, int32_t n_below, double prior_weight, int32_t lf) 
   a.msig = p->d_msig;
   a.info = p->d_info;
   a.coef = p->d_coef;
+  a.coef32 = p->d_coef32;
   a.kcap = p->kcap;
   a.ob = p->d_scratch;
   a.tmp = p->d_scratch;
@@ -1074,7 +1079,7 @@ int tpe_score(tpe_handle_t h, int32_t family, const double *x, int64_t n, const 
   if (rc) return rc;
   rc = put_mixture(h, p, 1, wa, ma, sa, ka, kind);
   if (rc) return rc;
-  CKH(launch_prep(p->d_hps, 1, p->d_mw, p->d_mmu, p->d_msig, p->d_info, p->d_coef, p->kcap,
+  CKH(launch_prep(p->d_hps, 1, p->d_mw, p->d_mmu, p->d_msig, p->d_info, p->d_coef, p->d_coef32, p->kcap,
                   p->d_scratch, h->stream));
   rc = ensure_ext(h, p, n);
   if (rc) return rc;
@@ -1122,7 +1127,7 @@ int tpe_sample(tpe_handle_t h, int32_t family, const double *w, const double *mu
   if (rc) return rc;
   rc = put_mixture(h, p, 1, w, mu, sigma, k, kind);
   if (rc) return rc;
-  CKH(launch_prep(p->d_hps, 1, p->d_mw, p->d_mmu, p->d_msig, p->d_info, p->d_coef, p->kcap,
+  CKH(launch_prep(p->d_hps, 1, p->d_mw, p->d_mmu, p->d_msig, p->d_info, p->d_coef, p->d_coef32, p->kcap,
                   p->d_scratch, h->stream));
   rc = ensure_ext(h, p, n);
   if (rc) return rc;
@@ -1470,7 +1475,7 @@ int tpe_plan_score_candidates_sorted(tpe_plan_t p, int32_t hp, int32_t mode, con
                                      int64_t *best_index, double *best_score) {
   if (!p) return TPE_E_INVALID;
   tpe_engine *h = p->eng;
-  if (hp < 0 || hp >= p->P || n < 0 || (n > 0 && !x) || mode < -1 || mode > 2)
+  if (hp < 0 || hp >= p->P || n < 0 || (n > 0 && !x) || mode < -1 || mode > 3)
     return fail(h, TPE_E_INVALID, "bad args");
   if (n > (int64_t)INT32_MAX) return fail(h, TPE_E_INVALID, "too many candidates");
   if (best_index) *best_index = -1;
@@ -1692,19 +1697,19 @@ static int lse_shift_min() {
 }
 
 int tpe_plan_set_prune(tpe_plan_t p, int32_t mode) {
-  if (!p || mode < 0 || mode > 2) return TPE_E_INVALID;
+  if (!p || mode < 0 || mode > 3) return TPE_E_INVALID;
   if (p->prune_mode != mode) graph_reset(p);
   p->prune_mode = mode;
   return TPE_OK;
 }
 
 int tpe_microbench(tpe_handle_t h, int32_t which, double *per_second) {
-  if (!h || !per_second || which < 0 || which > 5) return TPE_E_INVALID;
+  if (!h || !per_second || which < 0 || which > 6) return TPE_E_INVALID;
   CKH(hipSetDevice(h->device));
   hipDeviceProp_t prop;
   CKH(hipGetDeviceProperties(&prop, h->device));
   const int blocks = prop.multiProcessorCount * 8;
-  const int iters = which == 2 ? 256 : (which == 3 || which == 5 ? 512 : (which == 4 ? 128 : 4096));
+  const int iters = which == 2 ? 256 : (which == 3 || which >= 5 ? 512 : (which == 4 ? 128 : 4096));
   double *sink = nullptr;
   CKH(dalloc(&sink, (size_t)blocks * 256));
   hipEvent_t a, b;
@@ -1722,8 +1727,8 @@ int tpe_microbench(tpe_handle_t h, int32_t which, double *per_second) {
   dfree(sink);
   // results per thread-iteration: exp / FMA chains, erf chains, LSE pairs
   // (4 candidates x 8 components), quantized pairs (2 chains), shifted LSE
-  // pairs (4 x 8)
-  static const double per_iter[6] = {8.0, 16.0, 4.0, 32.0, 2.0, 32.0};
+  // pairs (4 x 8), block-local fp32 LSE pairs (4 x 8)
+  static const double per_iter[7] = {8.0, 16.0, 4.0, 32.0, 2.0, 32.0, 32.0};
   *per_second = 4.0 * blocks * 256.0 * iters * per_iter[which] / (ms * 1e-3);
   return TPE_OK;
 }

@@ -717,8 +717,9 @@ __device__ __forceinline__ Split compute_split(const FitArgs &A, const FitCtx &C
 // reduction per 8 components, computed with the coefficients) and the
 // padding components of the last block (alpha = -inf: terms exactly 0).
 // ------------------------------------------------------------------------
-__device__ __forceinline__ void store_table(const tpe_hp &H, Coef *cf, int K, const double *w, const double *mu,
-                            const double *sg, double pacc, bool quant) {
+__device__ __forceinline__ void store_table(const tpe_hp &H, Coef *cf, Coef32 *cf32, int K,
+                                            const double *w, const double *mu, const double *sg,
+                                            double pacc, bool quant) {
   const int kp = (K + kCoefBlock - 1) / kCoefBlock * kCoefBlock;
   // kp and the block size are multiples of 8: the 8 lanes of a block's
   // components are active together for the shuffles
@@ -728,7 +729,7 @@ __device__ __forceinline__ void store_table(const tpe_hp &H, Coef *cf, int K, co
     const Coef c = real ? make_coef(H, w[k], mu[k], sg[k], pacc, &e)
                         : Coef{-INFINITY, 0.0, 0.0, 0.0};
     store_coef(cf, k, c, quant);
-    if (!quant) store_lse_envelope(cf, k, e, real);
+    if (!quant) store_lse_envelope(cf, k, e, real, c, cf32);
   }
 }
 
@@ -739,10 +740,11 @@ __device__ __forceinline__ void store_table(const tpe_hp &H, Coef *cf, int K, co
 // (the descriptor comes by global pointer: a reference to a by-value copy
 // would put that copy on the scratch stack when the call is not inlined)
 __device__ __forceinline__ void prep_slot(const tpe_hp *Hg, int64_t slot, int K, const double *w, const double *mu,
-                          const double *sg, MixInfo *info, Coef *coef, int64_t kcap, double *tmp,
-                          FitShared &sm) {
+                          const double *sg, MixInfo *info, Coef *coef, Coef32 *coef32,
+                          int64_t kcap, double *tmp, FitShared &sm) {
   const tpe_hp H = *Hg;
   Coef *cf = coef + slot * kcap;
+  Coef32 *cf32 = coef32 + slot * (kcap / kCoefBlock);
   const double wsum = block_np_sum(w, K, sm);
   STAMP(7);
   if (H.family == TPE_CAT) {
@@ -769,7 +771,7 @@ __device__ __forceinline__ void prep_slot(const tpe_hp *Hg, int64_t slot, int K,
   }
   STAMP(8);
   const bool quant = (H.flags & TPE_HAS_Q) != 0;
-  store_table(H, cf, K, w, mu, sg, pacc, quant);
+  store_table(H, cf, cf32, K, w, mu, sg, pacc, quant);
   if (threadIdx.x == 0) {
     MixInfo mi;
     mi.K = K; mi.kind = quant ? 1 : 0; mi.p_accept = pacc; mi.log_pacc = log(pacc);
@@ -869,9 +871,10 @@ __device__ __forceinline__ void fit_continuous(const FitArgs &A, const FitCtx &C
   // per-component lpdf constants (tpe.py:138-160, 277-299) + copy-out
   const bool quant = (H.flags & TPE_HAS_Q) != 0;
   Coef *cf = A.coef + slot * A.kcap;
+  Coef32 *cf32 = A.coef32 + slot * (A.kcap / kCoefBlock);
   if (MIXLDS)
     for (int k = threadIdx.x; k < K; k += blockDim.x) { gw[k] = w[k]; gm[k] = mu[k]; gs[k] = sg[k]; }
-  store_table(H, cf, K, w, mu, sg, pacc, quant);
+  store_table(H, cf, cf32, K, w, mu, sg, pacc, quant);
   if (threadIdx.x == 0) {
     MixInfo mi;
     mi.K = K; mi.kind = quant ? 1 : 0; mi.p_accept = pacc; mi.log_pacc = log(pacc);
@@ -940,7 +943,8 @@ __device__ __forceinline__ void fit_categorical(const FitArgs &A, const FitCtx &
     sg[c] = 0.0;
   }
   __syncthreads();
-  prep_slot(A.hps + slot / 2, slot, upper, w, mu, sg, A.info, A.coef, A.kcap, A.tmp + slot * A.kcap, sm);
+  prep_slot(A.hps + slot / 2, slot, upper, w, mu, sg, A.info, A.coef, A.coef32, A.kcap,
+            A.tmp + slot * A.kcap, sm);
 }
 
 // ------------------------------------------------------------------------
@@ -1143,14 +1147,15 @@ __global__ __launch_bounds__(256) void k_prep(const tpe_hp *__restrict__ hps,
                                               const double *__restrict__ mmu,
                                               const double *__restrict__ msig,
                                               MixInfo *__restrict__ info, Coef *__restrict__ coef,
-                                              int64_t kcap, double *__restrict__ scratch) {
+                                              Coef32 *__restrict__ coef32, int64_t kcap,
+                                              double *__restrict__ scratch) {
   __shared__ FitShared sm;
   const int hp = blockIdx.x, side = blockIdx.y;
   const int64_t slot = 2 * (int64_t)hp + side;
   const int K = info[slot].K;
   __syncthreads();
-  prep_slot(hps + hp, slot, K, mw + slot * kcap, mmu + slot * kcap, msig + slot * kcap, info, coef, kcap,
-            scratch + slot * kcap, sm);
+  prep_slot(hps + hp, slot, K, mw + slot * kcap, mmu + slot * kcap, msig + slot * kcap, info, coef,
+            coef32, kcap, scratch + slot * kcap, sm);
 }
 
 // ------------------------------------------------------------------------
@@ -1183,10 +1188,10 @@ hipError_t launch_split(const FitArgs &a, uint8_t *below, hipStream_t st) {
 }
 
 hipError_t launch_prep(const tpe_hp *hps, int32_t n_hp, const double *mw, const double *mmu,
-                       const double *msig, MixInfo *info, Coef *coef, int64_t kcap,
-                       double *scratch, hipStream_t st) {
+                       const double *msig, MixInfo *info, Coef *coef, Coef32 *coef32,
+                       int64_t kcap, double *scratch, hipStream_t st) {
   if (n_hp <= 0) return hipSuccess;
-  k_prep<<<dim3(n_hp, 2), 256, 0, st>>>(hps, mw, mmu, msig, info, coef, kcap, scratch);
+  k_prep<<<dim3(n_hp, 2), 256, 0, st>>>(hps, mw, mmu, msig, info, coef, coef32, kcap, scratch);
   return hipGetLastError();
 }
 

@@ -112,6 +112,21 @@ __device__ __forceinline__ void store_coef(Coef *table, int64_t k, const Coef &c
   if (with_w) t[coef_off(k, 3)] = c.w;
 }
 
+// The same log-sum-exp terms per block of kCoefBlock components in
+// block-local fp32 form (prune mode 3, tpe_score.hip lse_chunks_shifted):
+//   t_k = A + alpha_k + u (beta_k + gamma_k u),  u = y' - center,
+// center = the block's mu' midpoint (fp64), A = an integer near the block's
+// largest alpha (so alpha_k stays small and exact to ~2^-24 absolute).  One
+// 128-B block = two 64-B scalar loads.
+struct __attribute__((aligned(128))) Coef32 {
+  double center;
+  float base;
+  float pad0;
+  float a[kCoefBlock], b[kCoefBlock], c[kCoefBlock];
+  float pad1[4];
+};
+static_assert(sizeof(Coef32) == 128, "two 64-B scalar loads");
+
 struct Partial {  // == tpe_result layout
   double score;
   double value;
@@ -147,6 +162,7 @@ struct ScoreArgs {
   const int32_t *cond_branch;
   const MixInfo *info;       // [2*P]
   const Coef *coef;          // [2*P][kcap]
+  const Coef32 *coef32;      // [2*P][kcap / kCoefBlock] block-local fp32 LSE terms
   const double *mw, *mmu, *msig;  // [2*P][kcap] (sampler reads side 0)
   const uint64_t *seeds;     // [S]
   const double *cand;        // candidates [S][n_slots][n_cand] (drawn or external)
@@ -203,6 +219,7 @@ struct FitArgs {
   double *mw, *mmu, *msig;   // [2P][kcap] fitted mixtures
   MixInfo *info;             // [2P]
   Coef *coef;                // [2P][kcap]
+  Coef32 *coef32;            // [2P][kcap / kCoefBlock]
   int64_t kcap;
   double *ob;                // [2P][kcap] scratch: observations of the slot
   double *tmp;               // [2P][kcap] scratch (may alias ob)
@@ -220,7 +237,7 @@ bool is_sorted_draw_kernel_fn(const void *f);
 const void *lattice_draw_kernel_fn();      // k_lattice<true> (lattice + fused draw)
 hipError_t launch_prep(const tpe_hp *hps, int32_t n_hp, const double *mw,
                        const double *mmu, const double *msig, MixInfo *info,
-                       Coef *coef, int64_t kcap, double *scratch,
+                       Coef *coef, Coef32 *coef32, int64_t kcap, double *scratch,
                        hipStream_t st);
 hipError_t launch_score(const ScoreArgs &a, bool has_erf, hipStream_t st);
 // lpdf pairs of every lattice point of the first n_lat hps of a level

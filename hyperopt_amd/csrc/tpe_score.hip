@@ -98,6 +98,33 @@ __device__ __forceinline__ void load_group(KDbl *__restrict__ cs, int k, CoefGro
   }
 }
 
+// prune mode 3: the block-local fp32 form of the same terms (Coef32)
+typedef const Coef32 __attribute__((address_space(4))) KC32;
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ KC32 *uniform_ptr32(const Coef32 *p) {
+  const uint64_t u = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  return (KC32 *)(((uint64_t)hi << 32) | lo);
+}
+struct CoefGroup32 {
+  double m;
+  float A;
+  float a[kGroup], b[kGroup], c[kGroup];
+};
+// two 64-B scalar loads: the block of component k
+__device__ __forceinline__ void load_group32(KC32 *__restrict__ t, int k, CoefGroup32 &g) {
+  KC32 *b = t + k / kCoefBlock;
+  g.m = b->center;
+  g.A = b->base;
+#pragma unroll
+  for (int j = 0; j < kGroup; ++j) {
+    g.a[j] = b->a[j];
+    g.b[j] = b->b[j];
+    g.c[j] = b->c[j];
+  }
+}
+
 // Single-pass log-sum-exp over the wave's chunks of a mixture of nb
 // components against the lane's KR candidates (log2 units, t = alpha +
 // y'(beta + gamma y'), make_coef).  Per group of kGroup components: the group
@@ -295,12 +322,38 @@ __device__ __forceinline__ void lse_fold_shifted(const float (&d)[KR][kGroup], d
   }
 }
 
-template <int KR, bool CENSUS, int STRIDE = kWaves>
+// Mode 3: t - M of the block in fp32, u = fp32(y' - center) once per
+// (candidate, block), then t - M = fma(fma(gamma, u, beta), u, (A - M) +
+// alpha) on packed fp32 pairs of components (v_pk_fma_f32): the fp64 FMAs
+// and the cvt of every pair become half a packed FMA each.  A - M is an
+// exact integer difference and alpha, beta u, gamma u^2 are O(1) for the
+// terms that matter, so the rounding stays at the level of the fp32 t - M
+// the fp64 form feeds v_exp_f32 (tools/fp32_pair_error.py: max 2.4e-8
+// relative lpdf error at config 4 against 1.2e-8 for the fp64 form).
+template <int KR>
+__device__ __forceinline__ void lse_terms_f32(const CoefGroup32 &g, float Mf,
+                                              const double (&y)[KR], float (&d)[KR][kGroup]) {
+  const float am = g.A - Mf;
+#pragma unroll
+  for (int r = 0; r < KR; ++r) {
+    const float u = (float)(y[r] - g.m);
+    const f2v u2 = {u, u}, am2 = {am, am};
+#pragma unroll
+    for (int j = 0; j < kGroup; j += 2) {
+      const f2v a2 = {g.a[j], g.a[j + 1]}, b2 = {g.b[j], g.b[j + 1]}, c2 = {g.c[j], g.c[j + 1]};
+      const f2v t = __builtin_elementwise_fma(__builtin_elementwise_fma(c2, u2, b2), u2, a2 + am2);
+      d[r][j] = t.x;
+      d[r][j + 1] = t.y;
+    }
+  }
+}
+
+template <int KR, bool CENSUS, int STRIDE = kWaves, bool F32 = false>
 __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
                                                    const Coef *__restrict__ cv, int c0, int nb,
                                                    const double (&y)[KR], const bool (&valid)[KR],
                                                    LseAcc (&out)[KR], LseWindow win, int nvalid,
-                                                   LseCensus &cen) {
+                                                   LseCensus &cen, KC32 *__restrict__ c32 = nullptr) {
   const int lane = threadIdx.x & 63;
   const int nch = (nb + kChunk - 1) / kChunk;
   const double *tb = reinterpret_cast<const double *>(cv);
@@ -393,15 +446,29 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
       // software-pipelined as in lse_chunks
       int kg = 0;
       bool have = next_live<STRIDE>(m0, m1, r0, kg);
-      CoefGroup cgp;
-      if (have) load_group(cs, kg, cgp);
-      while (have) {
-        float d[KR][kGroup];
-        lse_terms_shifted<KR>(cgp, M, y, y2, d);
-        have = next_live<STRIDE>(m0, m1, r0, kg);
-        load_group(cs, kg, cgp);
-        __builtin_amdgcn_sched_barrier(0);
-        lse_fold_shifted<KR>(d, s);
+      if constexpr (F32) {
+        const float Mf = (float)M;  // an integer (< 2^24 in magnitude): exact
+        CoefGroup32 g32;
+        if (have) load_group32(c32, kg, g32);
+        while (have) {
+          float d[KR][kGroup];
+          lse_terms_f32<KR>(g32, Mf, y, d);
+          have = next_live<STRIDE>(m0, m1, r0, kg);
+          load_group32(c32, kg, g32);
+          __builtin_amdgcn_sched_barrier(0);
+          lse_fold_shifted<KR>(d, s);
+        }
+      } else {
+        CoefGroup cgp;
+        if (have) load_group(cs, kg, cgp);
+        while (have) {
+          float d[KR][kGroup];
+          lse_terms_shifted<KR>(cgp, M, y, y2, d);
+          have = next_live<STRIDE>(m0, m1, r0, kg);
+          load_group(cs, kg, cgp);
+          __builtin_amdgcn_sched_barrier(0);
+          lse_fold_shifted<KR>(d, s);
+        }
       }
     }
     bool ok = true;
@@ -727,11 +794,16 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
         // smaller ones keep the exact per-group lift below)
         constexpr int ST = WT ? 1 : kWaves;
         const int cw0 = WT ? 0 : wv;
-        const bool shifted = prune && A.lse_prune > 1 && K >= A.lse_shift_min &&
-                             win.thr > -INFINITY &&
-                             lse_chunks_shifted<KR, CENSUS, ST>(uniform_ptr(cm), cm, cw0, K, y,
-                                                                valid, lacc[mix], win, nvalid,
-                                                                lcen);
+        bool shifted = false;
+        if (prune && A.lse_prune > 1 && K >= A.lse_shift_min && win.thr > -INFINITY) {
+          if (A.lse_prune > 2)  // block-local fp32 pairs (Coef32)
+            shifted = lse_chunks_shifted<KR, CENSUS, ST, true>(
+                uniform_ptr(cm), cm, cw0, K, y, valid, lacc[mix], win, nvalid, lcen,
+                uniform_ptr32(A.coef32 + (mix ? sa : sb) * (A.kcap / kCoefBlock)));
+          else
+            shifted = lse_chunks_shifted<KR, CENSUS, ST>(uniform_ptr(cm), cm, cw0, K, y, valid,
+                                                         lacc[mix], win, nvalid, lcen);
+        }
         if (!shifted) {
           if constexpr (WT) {
             // the exact loop in the 8-wave tile's association: chunk owner

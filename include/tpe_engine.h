@@ -232,7 +232,8 @@ int tpe_plan_score_candidates(tpe_plan_t p, int32_t hp, const double *x,
  * candidates are value-bucketed in blocks of TPE_SHARD_ALIGN exactly as
  * k_draw_sorted buckets its draws, then scored on the same tiles with
  * log-sum-exp prune mode `mode` (tpe_plan_set_prune: 0 every pair, 1 block
- * skip, 2 block skip + one exponent per wave).  Outputs are in the given
+ * skip, 2 block skip + one exponent per wave, 3 the same in block-local
+ * fp32).  Outputs are in the given
  * order.  The parity path of tpe.py:139-144 / 253-256 as the suggest
  * computes it at config 4.                                                 */
 int tpe_plan_score_candidates_sorted(tpe_plan_t p, int32_t hp, int32_t mode,
@@ -288,18 +289,22 @@ int tpe_plan_sample_prior(tpe_plan_t p, const uint64_t *seeds, int64_t n_suggest
 /* Large draws score log-sum-exp candidates on value-bucketed tiles.  mode 1
  * skips the blocks of 8 mixture components whose every term is below
  * 2^-(31 + log2 K) of each candidate's largest one (lpdf moved by <= 2^-30
- * ~ 1e-9 relative); mode 2 (default) also gives each wave one exponent
- * instead of a per-group max (terms 2^(t - M), M an upper bound of the
- * wave's terms), guarded so no term's fp32 argument exceeds ~|4| where it
- * matters (<= 3e-7 relative; else the wave falls back to mode 1).  mode 0
- * evaluates every (candidate, component) pair -- A/B measurement, tests.   */
+ * ~ 1e-9 relative); mode 2 also gives each wave one exponent instead of a
+ * per-group max (terms 2^(t - M), M an upper bound of the wave's terms),
+ * guarded so no term's fp32 argument exceeds ~|4| where it matters (<= 3e-7
+ * relative; else the wave falls back to mode 1); mode 3 (default) computes
+ * mode 2's t - M in fp32 about each component block's own centre (packed
+ * fp32 FMAs instead of fp64 ones; the exponent difference is exact, the
+ * rest O(1), so the error stays at mode 2's level).  mode 0 evaluates every
+ * (candidate, component) pair -- A/B measurement, tests.                    */
 int tpe_plan_set_prune(tpe_plan_t p, int32_t mode);
 
 /* Register-only microbenchmarks for the roofline: which = 0 v_exp_f32
  * (results/s), 1 fp64 FMA (flop/s), 2 OCML fp64 erf (results/s), 3 the
  * log-sum-exp (candidate, component) pair of the scoring kernel (pairs/s),
  * 4 a live quantized pair (2 fp64 erf; pairs/s), 5 the log-sum-exp pair of
- * the one-exponent-per-wave loop (tpe_plan_set_prune mode 2; pairs/s).      */
+ * the one-exponent-per-wave loop (tpe_plan_set_prune mode 2; pairs/s), 6 the
+ * same pair in block-local fp32 (mode 3; pairs/s).                          */
 int tpe_microbench(tpe_handle_t h, int32_t which, double *per_second);
 
 #ifdef __cplusplus

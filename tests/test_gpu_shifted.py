@@ -4,7 +4,8 @@ At config 4 almost every evaluated (candidate, component) pair runs in the
 large-draw form: candidates value-bucketed in 4096-candidate blocks
 (k_draw_sorted), log-sum-exp component blocks whose terms are provably below
 2^-(31 + log2 K) of the lane maximum skipped, and one exponent per wave
-(prune mode 2, ``lse_chunks_shifted``).  These tests anchor that form to the
+(``lse_chunks_shifted``: prune mode 2 with an fp64 quadratic, mode 3 -- the
+default -- with the block-local fp32 quadratic).  These tests anchor that form to the
 CPU oracle (the float64 restatement of tpe.py:104-166 / 259-301 with
 ``logsum_rows`` tpe.py:253-256, pinned to the reference by
 tests/test_oracle_golden.py):
@@ -17,7 +18,7 @@ tests/test_oracle_golden.py):
 * the full 1e7-candidate config-4 suggest: each of the 100 winners rescored
   by the oracle, the winner's value regenerated from its global index
   (tpe_sample at offset = index: broadcast_best returns samples[best],
-  tpe.py:756-757), and prune mode 2 against the exhaustive mode 0;
+  tpe.py:756-757), and prune modes 3 and 2 against the exhaustive mode 0;
 * the same value/index check on config 2 at 2^18 candidates (sorted draws).
 
 Tolerance (north star): |lpdf - oracle| <= 1e-6 * max(1, |oracle|); argmax
@@ -118,13 +119,13 @@ def _check_winners(dom, plan, res, seed, n, obs, key):
 # ---------------------------------------------------------------------------
 def test_config4_reference_candidates_production_form(cfg4_plan):
     """suggest_cfg4.npz's candidates (4096 per hp, drawn by the reference
-    from the below posterior) through the bucketed path in prune modes 1
-    and 2: lliks within 1e-6 of the reference's, argmax equivalent, and the
-    one-exponent form demonstrably ran (census)."""
+    from the below posterior) through the bucketed path in prune modes 1,
+    2 and 3: lliks within 1e-6 of the reference's, argmax equivalent, and
+    the one-exponent form demonstrably ran (census)."""
     dom, plan = cfg4_plan
     meta = load_json('suggest_big_meta.json')['cfg4']
     d = load('suggest_cfg4.npz')
-    for mode in (1, 2):
+    for mode in (1, 2, 3):
         plan.census(True)
         stats = {}
         for k, lab in enumerate(meta['labels']):
@@ -144,7 +145,7 @@ def test_config4_reference_candidates_production_form(cfg4_plan):
                                     plan.mixture(dom.space.by_label[l].index, 1)[0].size)
                             for l in meta['labels'])
         assert 0 < evaluated < total
-        if mode == 2:
+        if mode >= 2:
             assert shifted > 0.9 * evaluated, census     # the one-exponent form ran
         else:
             assert shifted == 0
@@ -183,7 +184,7 @@ def test_shifted_form_every_lse_kind_vs_oracle(lse_plan):
     """GMM (bounded, unbounded) and LGMM (bounded, unbounded) at K ~ 1e4:
     8192 draws of the below posterior plus 4096 spread over the prior range
     (the tails, where the guard and the skip thresholds are tightest),
-    scored through the bucketed path in modes 1 and 2 against the oracle."""
+    scored through the bucketed path in modes 1, 2 and 3 against the oracle."""
     dom, plan, obs = lse_plan
     tabs = dom.space.engine_tables()[0]
     rs = np.random.RandomState(3)
@@ -206,7 +207,7 @@ def test_shifted_form_every_lse_kind_vs_oracle(lse_plan):
                            math.exp(hi) if t.family == E.LGMM else hi)
         x = np.concatenate([x, wide])
         ref = _oracle_score(dom, obs, h.label, x)
-        for mode in (1, 2):
+        for mode in (1, 2, 3):
             plan.census(True)
             lb, la, bi, bs = plan.score_candidates(i, x, sorted_mode=mode)
             census = plan.census(False)
@@ -214,7 +215,7 @@ def test_shifted_form_every_lse_kind_vs_oracle(lse_plan):
             assert_close(la, ref['llik_a'], msg='%s above, mode %d' % (h.label, mode))
             with np.errstate(all='ignore'):
                 assert argmax_equiv(ref['llik_b'] - ref['llik_a'], bi), (h.label, mode)
-            if mode == 2:
+            if mode >= 2:
                 assert census[4] > 0, (h.label, census)
             _record('lse_%s_mode%d' % (h.label, mode), census=list(census),
                     below=_delta(lb, ref['llik_b']), above=_delta(la, ref['llik_a']))
@@ -231,38 +232,42 @@ def test_shifted_form_suggest_winners_vs_oracle(lse_plan):
 
 
 def test_config4_full_suggest_winners_vs_oracle(cfg4_plan):
-    """The bench workload (config 4, 1e7 candidates per hp, default prune
-    mode 2): every winner's value is the draw at its reported global index,
-    and its score is the oracle's lpdf difference at that value within 1e-6.
-    Mode 0 (every pair, exact per-group lift) on the same draw: same winners
-    up to 1e-6 EI ties, and each mode-2 winner scores (by the oracle) within
-    1e-6 of the mode-0 winner."""
+    """The bench workload (config 4, 1e7 candidates per hp; the default
+    prune mode 3, and mode 2): every winner's value is the draw at its
+    reported global index, and its score is the oracle's lpdf difference at
+    that value within 1e-6.  Mode 0 (every pair, exact per-group lift) on
+    the same draw: same winners up to 1e-6 EI ties, and each pruned winner
+    scores (by the oracle) within 1e-6 of the mode-0 winner."""
     dom, plan = cfg4_plan
     _, L, vals, act = big_configs.cfg4_domain_history(hp, Domain)
     obs = _oracle_obs(dom, L, vals, act)
     n, seed = 10_000_000, 7
-    res2 = plan.suggest([seed], n)[0]
-    dev2, orc2 = _check_winners(dom, plan, res2, seed, n, obs, 'cfg4 mode 2')
+    res, dev, orc = {}, {}, {}
     try:
-        plan.set_prune(0)
-        res0 = plan.suggest([seed], n)[0]
+        for mode in (3, 2, 0):
+            plan.set_prune(mode)
+            res[mode] = plan.suggest([seed], n)[0]
+            dev[mode], orc[mode] = _check_winners(dom, plan, res[mode], seed, n, obs,
+                                                  'cfg4 mode %d' % mode)
     finally:
-        plan.set_prune(2)
-    dev0, orc0 = _check_winners(dom, plan, res0, seed, n, obs, 'cfg4 mode 0')
-    same = res2['index'] == res0['index']
-    np.testing.assert_array_equal(res2['value'][same], res0['value'][same])
-    d_same = np.abs(res2['score'][same] - res0['score'][same])
-    assert (d_same <= RTOL * np.maximum(1.0, np.abs(res0['score'][same]))).all()
-    orc2, orc0 = np.asarray(orc2), np.asarray(orc0)
-    # the mode-2 winner is an argmax within tolerance: the oracle ranks it at
-    # most 1e-6 below the exhaustive run's winner (and vice versa)
-    gap = orc0 - orc2
-    assert (np.abs(gap) <= RTOL * np.maximum(1.0, np.abs(orc0))).all(), gap.max()
-    _record('cfg4_full_suggest', mode2_winner_vs_oracle=_delta(dev2, orc2),
-            mode0_winner_vs_oracle=_delta(dev0, orc0),
-            mode2_vs_mode0_same_index=dict(n=int(same.sum()),
-                                           max_abs=float(d_same.max()) if d_same.size else 0.0),
-            tied_swaps=int((~same).sum()), max_oracle_gap=float(np.abs(gap).max()))
+        plan.set_prune(3)
+    rec = {'mode0_winner_vs_oracle': _delta(dev[0], orc[0])}
+    for mode in (3, 2):
+        same = res[mode]['index'] == res[0]['index']
+        np.testing.assert_array_equal(res[mode]['value'][same], res[0]['value'][same])
+        d_same = np.abs(res[mode]['score'][same] - res[0]['score'][same])
+        assert (d_same <= RTOL * np.maximum(1.0, np.abs(res[0]['score'][same]))).all()
+        o, o0 = np.asarray(orc[mode]), np.asarray(orc[0])
+        # the pruned winner is an argmax within tolerance: the oracle ranks it
+        # at most 1e-6 below the exhaustive run's winner (and vice versa)
+        gap = o0 - o
+        assert (np.abs(gap) <= RTOL * np.maximum(1.0, np.abs(o0))).all(), gap.max()
+        rec['mode%d_winner_vs_oracle' % mode] = _delta(dev[mode], orc[mode])
+        rec['mode%d_vs_mode0_same_index' % mode] = dict(
+            n=int(same.sum()), max_abs=float(d_same.max()) if d_same.size else 0.0)
+        rec['mode%d_tied_swaps' % mode] = int((~same).sum())
+        rec['mode%d_max_oracle_gap' % mode] = float(np.abs(gap).max())
+    _record('cfg4_full_suggest', **rec)
 
 
 def test_config2_sorted_draw_winner_values_regenerate():

@@ -414,8 +414,9 @@ def test_pruned_lse_equals_full_evaluation(name):
     log-sum-exp tiles skip the component blocks whose terms are all below
     2^-(31 + log2 K) of every candidate's largest (mode 1): winners (index,
     value) equal the unpruned run and scores agree within 2^-30 relative per
-    lpdf.  Mode 2 (default) also gives each wave one exponent: scores within
-    the north-star 1e-6, winners equal up to ties within it.  The winner also
+    lpdf.  Modes 2 and 3 (default) also give each wave one exponent (fp64 /
+    block-local fp32 quadratic): scores within the north-star 1e-6, winners
+    equal up to ties within it.  The winner also
     equals the merge of two differently tiled shards."""
     torch = pytest.importorskip('torch')
     from gpu_util import assert_winners_match
@@ -428,15 +429,18 @@ def test_pruned_lse_equals_full_evaluation(name):
     got = plan.suggest([21, 22], n)
     c = plan.census(False)
     plan.set_prune(2)
+    shifted64 = plan.suggest([21, 22], n)
+    plan.set_prune(3)
     shifted = plan.suggest([21, 22], n)
     plan.set_prune(0)
     want = plan.suggest([21, 22], n)
-    plan.set_prune(2)
+    plan.set_prune(3)
     np.testing.assert_array_equal(got['index'], want['index'])
     np.testing.assert_array_equal(got['value'], want['value'])
     np.testing.assert_array_equal(got['active'], want['active'])
     np.testing.assert_allclose(got['score'], want['score'], rtol=4e-9, atol=4e-9)
-    assert_winners_match(shifted, want, msg='one exponent per wave')
+    assert_winners_match(shifted64, want, msg='one exponent per wave')
+    assert_winners_match(shifted, want, msg='one exponent per wave, block-local fp32')
     assert c[3] > 0 and c[5] < c[3], c          # blocks were skipped
     if name != 'cfg2':
         return                                   # one level: shards merge directly
