@@ -209,6 +209,7 @@ __device__ __forceinline__ void store_lse_envelope(Coef *table, int64_t k, EnvTe
   bad |= dpp<kDppHalfMirror>((int)bad) != 0;
   // block-local fp32 form (Coef32): expand the quadratic about the block's
   // mu' midpoint in fp64, alpha relative to an integer block base
+  bool wide = false;
   {
     const double cen = (lo <= hi) ? 0.5 * (lo + hi) : 0.0;
     const double al = valid ? cf.x + cen * (cf.y + cen * cf.z) : -INFINITY;
@@ -218,6 +219,14 @@ __device__ __forceinline__ void store_lse_envelope(Coef *table, int64_t k, EnvTe
     amax = fmax(amax, dppd<kDppXor2>(amax));
     amax = fmax(amax, dppd<kDppHalfMirror>(amax));
     const double base = (amax > -1.0e300 && amax < 1.0e300) ? floor(amax) : 0.0;
+    // spread a^2 (mu' - centre)^2 of the block (NaN / inf: keep fp64 too)
+    const double dm = e.m - cen;
+    double sp = valid ? e.a2 * dm * dm : 0.0;
+    if (!(sp <= kF32Spread)) sp = INFINITY;
+    sp = fmax(sp, dppd<kDppXor1>(sp));
+    sp = fmax(sp, dppd<kDppXor2>(sp));
+    sp = fmax(sp, dppd<kDppHalfMirror>(sp));
+    wide = !(sp <= kF32Spread);
     Coef32 *b = t32 + k / kCoefBlock;
     const int j = (int)(k % kCoefBlock);
     b->a[j] = (float)(al - base);
@@ -237,6 +246,7 @@ __device__ __forceinline__ void store_lse_envelope(Coef *table, int64_t k, EnvTe
   out[2] = ((double)fc < cm) ? nextafterf(fc, INFINITY) : fc;
   out[3] = ((double)fa > am) ? nextafterf(fa, 0.0f) : fa;
   if (bad) { out[2] = INFINITY; out[3] = 0.0f; }
+  if (wide) out[3] = -out[3];  // the block keeps the fp64 quadratic in mode 3
 }
 
 }  // namespace tpe

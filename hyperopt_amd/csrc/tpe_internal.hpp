@@ -116,8 +116,14 @@ __device__ __forceinline__ void store_coef(Coef *table, int64_t k, const Coef &c
 // block-local fp32 form (prune mode 3, tpe_score.hip lse_chunks_shifted):
 //   t_k = A + alpha_k + u (beta_k + gamma_k u),  u = y' - center,
 // center = the block's mu' midpoint (fp64), A = an integer near the block's
-// largest alpha (so alpha_k stays small and exact to ~2^-24 absolute).  One
-// 128-B block = two 64-B scalar loads.
+// largest alpha (so alpha_k stays small and exact to ~2^-24 absolute).  The
+// form is exact to fp32 rounding of O(1) parts only while every component
+// sits within ~1 of its own scale from the centre (a_k^2 (mu'_k - centre)^2
+// <= kF32Spread): blocks that straddle a gap between tight clusters (small
+// sigma, wide block) are flagged -- the sign bit of their envelope's a^2
+// (kLseDeadBase) -- and keep the fp64 quadratic.  One 128-B block = two 64-B
+// scalar loads.
+constexpr double kF32Spread = 1.0;
 struct __attribute__((aligned(128))) Coef32 {
   double center;
   float base;

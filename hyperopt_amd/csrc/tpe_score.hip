@@ -206,7 +206,7 @@ struct LseCensus {
 // largest term any of its components can reach there (log2 units).
 __device__ __forceinline__ float envelope_bound(const float4 e, const LseWindow &win) {
   const float d = fmaxf(0.0f, fmaxf(e.x - win.hi, win.lo - e.y));
-  return fmaf(-e.w, d * d, e.z);
+  return fmaf(-fabsf(e.w), d * d, e.z);  // (the sign of e.w flags a wide block, Coef32)
 }
 
 // The wave's chunks c = c0 (mod kWaves) of a mixture of nb components, in
@@ -421,13 +421,16 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
       const int c = r0 + STRIDE * lane;
       const int k0 = c * kChunk;
       const bool has0 = c < nch, has1 = has0 && k0 + kGroup < nb;
-      bool live0 = false, live1 = false;
+      bool live0 = false, live1 = false, wide0 = false, wide1 = false;
       if (has0) {
-        live0 =
-            envelope_bound(*reinterpret_cast<const float4 *>(tb + coef_off(k0, 3)), win) >= win.thr;
-        if (has1)
-          live1 = envelope_bound(*reinterpret_cast<const float4 *>(tb + coef_off(k0 + kGroup, 3)),
-                                 win) >= win.thr;
+        const float4 e0 = *reinterpret_cast<const float4 *>(tb + coef_off(k0, 3));
+        live0 = envelope_bound(e0, win) >= win.thr;
+        wide0 = __builtin_signbit(e0.w);
+        if (has1) {
+          const float4 e1 = *reinterpret_cast<const float4 *>(tb + coef_off(k0 + kGroup, 3));
+          live1 = envelope_bound(e1, win) >= win.thr;
+          wide1 = __builtin_signbit(e1.w);
+        }
       }
       if constexpr (CENSUS) {
         const int n0 = has0 ? min(kGroup, nb - k0) : 0,
@@ -442,7 +445,9 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
         cen.exec += ex * (uint32_t)nvalid;
         cen.shift += ex * (uint32_t)nvalid;
       }
-      uint64_t m0 = __ballot(live0), m1 = __ballot(live1);
+      // (mode 3: the live wide blocks -- kF32Spread, flagged by the sign of
+      // their envelope's a^2 -- go to a second, fp64 loop after the round)
+      uint64_t m0 = __ballot(live0 && !(F32 && wide0)), m1 = __ballot(live1 && !(F32 && wide1));
       // software-pipelined as in lse_chunks
       int kg = 0;
       bool have = next_live<STRIDE>(m0, m1, r0, kg);
@@ -456,6 +461,14 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
           have = next_live<STRIDE>(m0, m1, r0, kg);
           load_group32(c32, kg, g32);
           __builtin_amdgcn_sched_barrier(0);
+          lse_fold_shifted<KR>(d, s);
+        }
+        uint64_t x0 = __ballot(live0 && wide0), x1 = __ballot(live1 && wide1);
+        while (next_live<STRIDE>(x0, x1, r0, kg)) {
+          CoefGroup g;
+          load_group(cs, kg, g);
+          float d[KR][kGroup];
+          lse_terms_shifted<KR>(g, M, y, y2, d);
           lse_fold_shifted<KR>(d, s);
         }
       } else {

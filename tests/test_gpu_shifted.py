@@ -221,6 +221,51 @@ def test_shifted_form_every_lse_kind_vs_oracle(lse_plan):
                     below=_delta(lb, ref['llik_b']), above=_delta(la, ref['llik_a']))
 
 
+def test_shifted_form_clustered_history_vs_oracle():
+    """A history of tight clusters with wide gaps (K_a ~ 1e4, sigmas at the
+    prior_sigma / 100 floor): the coefficient blocks that straddle a gap put
+    components far from their block's centre in units of their own sigma,
+    where the block-local fp32 quadratic of mode 3 would cancel
+    catastrophically -- those blocks are flagged (kF32Spread) and keep the
+    fp64 quadratic.  Every mode against the oracle, candidates on and
+    between the clusters."""
+    dom = Domain(lambda x: 0.0, {'u': hp.uniform('u', -5, 5), 'n': hp.normal('n', 0.0, 3.0)})
+    rs = np.random.RandomState(17)
+    n = 10000
+    centres = np.array([-4.0, -1.5, 0.2, 3.0])
+    # 'n': four tight clusters; 'u': a dense half plus, in the other half,
+    # small tight clusters of 4 (a converged optimizer's repeats) among
+    # sparse points -- blocks holding both are wide, and a candidate at a
+    # small cluster takes its dominant terms from one such block
+    small = np.repeat(np.linspace(0.5, 4.5, 12), 4) + 1e-5 * rs.randn(48)
+    cols = {'n': centres[rs.randint(0, 4, n)] + 1e-4 * rs.randn(n),
+            'u': np.concatenate([rs.uniform(-5, 0, n - 48 - 40), small, rs.uniform(0, 5, 40)])}
+    rs.shuffle(cols['u'])
+    clusters = {'n': centres, 'u': np.concatenate([centres, np.linspace(0.5, 4.5, 12)])}
+    labels = dom.space.labels
+    vals = np.stack([cols[l] for l in labels])
+    L = np.random.RandomState(18).rand(n)
+    act = np.ones_like(vals, dtype=np.uint8)
+    hps, conds, pprior = dom.space.engine_tables()
+    plan = E.Plan(E.default_engine(), hps, conds, pprior, max_trials=n)
+    plan.set_history(L, vals, act)
+    plan.fit()
+    obs = _oracle_obs(dom, L, vals, act)
+    for h in dom.space.hps:
+        i = h.index
+        cc = clusters[h.label]
+        x = np.concatenate([cc[rs.randint(0, cc.size, 6000)] + 0.05 * rs.randn(6000),
+                            rs.uniform(-5, 5, 6000)])
+        x = np.clip(x, -5, 4.999999)
+        ref = _oracle_score(dom, obs, h.label, x)
+        for mode in (1, 2, 3):
+            lb, la, bi, bs = plan.score_candidates(i, x, sorted_mode=mode)
+            assert_close(lb, ref['llik_b'], msg='%s below, mode %d' % (h.label, mode))
+            assert_close(la, ref['llik_a'], msg='%s above, mode %d' % (h.label, mode))
+            _record('clustered_%s_mode%d' % (h.label, mode),
+                    below=_delta(lb, ref['llik_b']), above=_delta(la, ref['llik_a']))
+
+
 def test_shifted_form_suggest_winners_vs_oracle(lse_plan):
     """A 2^20-candidate suggest of the four-kind space (sorted draws, mode
     2): winners rescored by the oracle and regenerated from their index."""
