@@ -819,19 +819,16 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
         }
         if (!shifted) {
           if constexpr (WT) {
-            // the exact loop in the 8-wave tile's association: chunk owner
-            // v = c (mod kWaves) as 8 passes, merged in owner order -- the
-            // same sums, bit for bit, as the component-split tile's waves
-            for (int v = 0; v < kWaves; ++v) {
-              LseAcc part[KR];
-              lse_chunks<KR, CENSUS, kWaves>(uniform_ptr(cm), cm, v, K, y, part, prune, win,
-                                             nvalid, lcen);
-#pragma unroll
-              for (int r = 0; r < KR; ++r) {
-                if (v == 0) lacc[mix][r] = part[r];
-                else lse_merge(lacc[mix][r], part[r]);
-              }
-            }
+            // the exact per-group-lift loop over every chunk in order, one
+            // pass (64 consecutive chunks per envelope round).  (Round 2 ran
+            // it as 8 owner passes c = v (mod 8) merged in v order, the 8-wave
+            // tile's association: bit-identical to that tile, but 8 envelope
+            // rounds and lift states per mixture where a config-5 wave has
+            // ~3 live blocks per pass.  Nothing compares the two tile shapes
+            // bit for bit: batched, sharded and chunked runs of one draw take
+            // the same tile shape.)
+            lse_chunks<KR, CENSUS, 1>(uniform_ptr(cm), cm, 0, K, y, lacc[mix], prune, win, nvalid,
+                                      lcen);
           } else {
             lse_chunks<KR, CENSUS, kWaves>(uniform_ptr(cm), cm, wv, K, y, lacc[mix], prune, win,
                                            nvalid, lcen);
@@ -1032,10 +1029,14 @@ __device__ __forceinline__ void mark_inactive(const ScoreArgs &A, int s, int s0,
   }
 }
 
-template <bool ERFK, bool CENSUS>
-__global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(6)))
-void k_score(ScoreArgs A) {
-  __shared__ ScoreSmem sm;
+// The kinds a scoring kernel instantiates: every kind but the per-candidate
+// erf ones, every kind, or only the wave-tile log-sum-exp kinds (levels of
+// large draws whose every slot is one: a kernel with only their register
+// allocation -- the combined one keeps the most any kind needs).
+enum { kSetNoErf = 0, kSetAll = 1, kSetWave = 2 };
+
+template <int SET, bool CENSUS>
+__device__ __forceinline__ void score_block(const ScoreArgs &A, ScoreSmem &sm) {
   const int b = blockIdx.x;
   int g = 0;
   while (g + 1 < A.n_groups && b >= A.grp_block0[g + 1]) ++g;
@@ -1051,18 +1052,45 @@ void k_score(ScoreArgs A) {
     if (slot < 0) return;
   }
   const bool known = A.compact != 0;
-  switch (A.grp_kind[g]) {
-    case KIND_LSE_G: score_tile<KIND_LSE_G, CENSUS>(A, sm, slot, tile, nt, known); break;
-    case KIND_LSE_L: score_tile<KIND_LSE_L, CENSUS>(A, sm, slot, tile, nt, known); break;
-    case KIND_LSE_G1: score_tile<KIND_LSE_G1, CENSUS>(A, sm, slot, tile, nt, known); break;
-    case KIND_LSE_L1: score_tile<KIND_LSE_L1, CENSUS>(A, sm, slot, tile, nt, known); break;
-    case KIND_LSE_GW: score_tile<KIND_LSE_GW, CENSUS>(A, sm, slot, tile, nt, known); break;
-    case KIND_LSE_LW: score_tile<KIND_LSE_LW, CENSUS>(A, sm, slot, tile, nt, known); break;
-    case KIND_ERF_G: if constexpr (ERFK) score_tile<KIND_ERF_G, CENSUS>(A, sm, slot, tile, nt, known); break;
-    case KIND_ERF_L: if constexpr (ERFK) score_tile<KIND_ERF_L, CENSUS>(A, sm, slot, tile, nt, known); break;
-    case KIND_LAT: score_tile<KIND_LAT, CENSUS>(A, sm, slot, tile, nt, known); break;
-    default: score_tile<KIND_CAT, CENSUS>(A, sm, slot, tile, nt, known); break;
+  if constexpr (SET == kSetWave) {
+    if (A.grp_kind[g] == KIND_LSE_LW) score_tile<KIND_LSE_LW, CENSUS>(A, sm, slot, tile, nt, known);
+    else score_tile<KIND_LSE_GW, CENSUS>(A, sm, slot, tile, nt, known);
+    return;
+  } else {
+    switch (A.grp_kind[g]) {
+      case KIND_LSE_G: score_tile<KIND_LSE_G, CENSUS>(A, sm, slot, tile, nt, known); break;
+      case KIND_LSE_L: score_tile<KIND_LSE_L, CENSUS>(A, sm, slot, tile, nt, known); break;
+      case KIND_LSE_G1: score_tile<KIND_LSE_G1, CENSUS>(A, sm, slot, tile, nt, known); break;
+      case KIND_LSE_L1: score_tile<KIND_LSE_L1, CENSUS>(A, sm, slot, tile, nt, known); break;
+      case KIND_LSE_GW: score_tile<KIND_LSE_GW, CENSUS>(A, sm, slot, tile, nt, known); break;
+      case KIND_LSE_LW: score_tile<KIND_LSE_LW, CENSUS>(A, sm, slot, tile, nt, known); break;
+      case KIND_ERF_G:
+        if constexpr (SET == kSetAll) score_tile<KIND_ERF_G, CENSUS>(A, sm, slot, tile, nt, known);
+        break;
+      case KIND_ERF_L:
+        if constexpr (SET == kSetAll) score_tile<KIND_ERF_L, CENSUS>(A, sm, slot, tile, nt, known);
+        break;
+      case KIND_LAT: score_tile<KIND_LAT, CENSUS>(A, sm, slot, tile, nt, known); break;
+      default: score_tile<KIND_CAT, CENSUS>(A, sm, slot, tile, nt, known); break;
+    }
   }
+}
+
+template <bool ERFK, bool CENSUS>
+__global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(6)))
+void k_score(ScoreArgs A) {
+  __shared__ ScoreSmem sm;
+  score_block<ERFK ? kSetAll : kSetNoErf, CENSUS>(A, sm);
+}
+
+#ifndef TPE_WAVE_EU
+#define TPE_WAVE_EU 6
+#endif
+template <bool CENSUS>
+__global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(TPE_WAVE_EU)))
+void k_score_wave(ScoreArgs A) {
+  __shared__ ScoreSmem sm;
+  score_block<kSetWave, CENSUS>(A, sm);
 }
 
 // Value-lattice scoring of the bounded quantized hps (KIND_LAT).  A drawn
@@ -1276,7 +1304,13 @@ hipError_t launch_score(const ScoreArgs &a, bool has_erf, hipStream_t st) {
   const int blocks = a.grp_block0[a.n_groups];
   if (blocks <= 0) return hipSuccess;
   const dim3 g((unsigned)blocks, a.n_suggest);
-  if (has_erf) {
+  bool wave_only = true;
+  for (int i = 0; i < a.n_groups; ++i)
+    wave_only &= a.grp_kind[i] == KIND_LSE_GW || a.grp_kind[i] == KIND_LSE_LW;
+  if (wave_only) {
+    if (a.census) k_score_wave<true><<<g, kWaves * 64, 0, st>>>(a);
+    else k_score_wave<false><<<g, kWaves * 64, 0, st>>>(a);
+  } else if (has_erf) {
     if (a.census) k_score<true, true><<<g, kWaves * 64, 0, st>>>(a);
     else k_score<true, false><<<g, kWaves * 64, 0, st>>>(a);
   } else {

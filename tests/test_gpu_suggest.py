@@ -303,9 +303,13 @@ def test_fit_suggest_matches_fit_then_suggest(name):
 
 
 def test_large_draw_grid_stride_matches_one_per_thread():
-    """Large draws take 8 candidates per thread (grid-stride k_draw), small
-    ones one; candidates are counter-based, so a 2^18-candidate suggest
-    (strided path) must equal the merge of two chunks drawn one per thread."""
+    """Large draws (>= 2^22 per launch) come out of k_draw_sorted and score
+    on pruned wave tiles; small ones are drawn one per thread and scored
+    unpruned on 8-wave tiles.  Candidates are counter-based, so a 2^18-
+    candidate suggest equals the merge of two small-draw chunks: the same
+    winners, or (the two tile shapes sum in different orders, and the large
+    one skips negligible blocks) ties within the scoring tolerance."""
+    from gpu_util import assert_winners_match
     torch = pytest.importorskip('torch')
     meta, d, dom, trials = _fixture_trials('cfg2')
     tpe.suggest([meta['new_id']], dom, trials, 7, n_EI_candidates=64)
@@ -317,8 +321,8 @@ def test_large_draw_grid_stride_matches_one_per_thread():
     raw = torch.from_numpy(np.stack(parts).view(np.uint8).reshape(-1).copy()).cuda()
     merged = plan.merge(raw.data_ptr(), world=2, level=0)
     torch.cuda.synchronize()
-    np.testing.assert_array_equal(merged['index'], full['index'])
-    np.testing.assert_array_equal(merged['value'], full['value'])
+    swaps = assert_winners_match(merged, full, msg='sorted large draw vs small-draw chunks')
+    assert swaps <= 2, swaps
 
 
 def test_graph_replay_in_child_process():
