@@ -481,18 +481,20 @@ def report(args, C, eng, world, mode, elapsed, value, pairs_step, pairs_suggest,
     # (one-exponent pairs: fp64 quadratic in prune mode 2, block-local fp32 in 3)
     lse_peak_exact = eng.microbench(3)
     lse_peak_shift = eng.microbench(6 if args.prune == 3 else 5)
+    lse_peak_exact32 = eng.microbench(7)   # mode 3's fp32 per-group-lift pair
     lse_peak = max(lse_peak_exact, lse_peak_shift)
     erf_peak = eng.microbench(4)
     lse_pairs = kinds.get('lse_gmm', 0.0) + kinds.get('lse_lgmm', 0.0)
     per_launch = max(1, launches)
     lse_exec = census[5] / per_launch if census[3] else lse_pairs
     lse_shift = census[4] / per_launch if census[3] else 0.0   # of which one-exponent form
+    lse_exact32 = census[6] / per_launch if census[3] else 0.0  # fp32 per-group-lift form
     erf_exec = census[2] / per_launch
     t_kernel = score_ms * 1e-3
     # each evaluated pair priced at the register-only rate of the arithmetic
     # it ran: per-group-max lift, one wave exponent, or quantized erf
-    t_peak = ((lse_exec - lse_shift) / lse_peak_exact + lse_shift / lse_peak_shift +
-              erf_exec / erf_peak)
+    t_peak = ((lse_exec - lse_shift - lse_exact32) / lse_peak_exact + lse_shift / lse_peak_shift +
+              lse_exact32 / lse_peak_exact32 + erf_exec / erf_peak)
     frac = t_peak / t_kernel if t_kernel else None
     achieved = (frac or 0.0) * lse_peak
     traffic = None
@@ -515,9 +517,12 @@ def report(args, C, eng, world, mode, elapsed, value, pairs_step, pairs_suggest,
                      'the fastest (one-exponent) LSE form; peaks are microkernels of exactly the '
                      'pair arithmetic (LSE pair: 2 fp64 FMA + cvt + v_exp_f32 + fp32/fp64 sum, '
                      'SURVEY 8d "1 exp + 6 flops"; prune mode 3 one-exponent pair: 1 packed '
-                     'fp32 FMA pair per 2 components + v_exp_f32 + sums; quantized pair: 2 OCML '
-                     'fp64 erf + 8 flops)',
+                     'fp32 FMA pair per 2 components + v_exp_f32 + sums; mode 3 per-group-lift '
+                     'pair below the one-exponent size: the same in fp32 with the group max and '
+                     'lift; quantized pair: 2 OCML fp64 erf + 8 flops)',
                 lse_evaluated_shifted_pairs_per_launch=lse_shift,
+                lse_evaluated_exact_f32_pairs_per_launch=lse_exact32,
+                lse_pair_max_lift_f32_peak_per_s=lse_peak_exact32,
                 lse_pairs_per_launch=lse_pairs, lse_evaluated_pairs_per_launch=lse_exec,
                 erf_pairs_per_launch=kinds.get('erf_gmm', 0.0) + kinds.get('erf_lgmm', 0.0),
                 erf_evaluated_pairs_per_launch=erf_exec,

@@ -40,7 +40,7 @@ EXPORTS = (
     'tpe_plan_profile', 'tpe_plan_profile_read', 'tpe_microbench', 'tpe_plan_get_results',
     'tpe_plan_results_device', 'tpe_plan_census', 'tpe_plan_fit_suggest',
     'tpe_plan_set_lattice', 'tpe_plan_update_history', 'tpe_plan_set_prune',
-    'tpe_plan_sample_prior', 'tpe_plan_score_candidates_sorted',
+    'tpe_plan_sample_prior', 'tpe_plan_score_candidates_sorted', 'tpe_plan_census_n',
 )
 
 # include/tpe_engine.h TPE_SHARD_ALIGN: candidate splits at multiples of this
@@ -151,6 +151,7 @@ def load_library(path: str = LIB_PATH):
             'tpe_plan_get_results': (C.c_int, [vp, vp, i32, vp]),
             'tpe_plan_results_device': (vp, [vp]),
             'tpe_plan_census': (C.c_int, [vp, i32, C.POINTER(i64)]),
+            'tpe_plan_census_n': (C.c_int, [vp, i32, C.POINTER(i64), i32]),
             'tpe_plan_set_lattice': (C.c_int, [vp, i32]),
             'tpe_plan_set_prune': (C.c_int, [vp, i32]),
             'tpe_plan_sample_prior': (C.c_int, [vp, C.POINTER(u64), i64, vp, i32, vp]),
@@ -529,11 +530,12 @@ class Plan(object):
     def census(self, enable):
         """Pair census since the last call: (quantized total, live, evaluated,
         log-sum-exp total, log-sum-exp evaluated in the one-exponent form,
-        log-sum-exp evaluated); enable it for the following suggests."""
+        log-sum-exp evaluated, of those in the fp32 per-group-lift form);
+        enable it for the following suggests."""
         e = self.engine
-        out = (C.c_int64 * 6)()
+        out = (C.c_int64 * 7)()
         with e.lock:
-            e.check(e.lib.tpe_plan_census(self.p, int(bool(enable)), out))
+            e.check(e.lib.tpe_plan_census_n(self.p, int(bool(enable)), out, 7))
         return tuple(int(v) for v in out)
 
     def last_stats(self):

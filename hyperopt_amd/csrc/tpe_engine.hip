@@ -1591,14 +1591,18 @@ int tpe_plan_set_lattice(tpe_plan_t p, int32_t enable) {
 }
 
 int tpe_plan_census(tpe_plan_t p, int32_t enable, int64_t *counts) {
-  if (!p) return TPE_E_INVALID;
+  return tpe_plan_census_n(p, enable, counts, 6);
+}
+
+int tpe_plan_census_n(tpe_plan_t p, int32_t enable, int64_t *counts, int32_t n_counts) {
+  if (!p || n_counts < 0) return TPE_E_INVALID;
   tpe_engine *h = p->eng;
   CKH(hipSetDevice(h->device));
   CKH(hipDeviceSynchronize());
   if (counts) {
     unsigned long long c[kCensus];
     CKH(hipMemcpy(c, p->d_census, sizeof(c), hipMemcpyDeviceToHost));
-    for (int i = 0; i < kCensus; ++i) counts[i] = (int64_t)c[i];
+    for (int i = 0; i < kCensus && i < n_counts; ++i) counts[i] = (int64_t)c[i];
   }
   CKH(hipMemset(p->d_census, 0, kCensus * sizeof(unsigned long long)));
   p->census = enable != 0;
@@ -1704,7 +1708,7 @@ int tpe_plan_set_prune(tpe_plan_t p, int32_t mode) {
 }
 
 int tpe_microbench(tpe_handle_t h, int32_t which, double *per_second) {
-  if (!h || !per_second || which < 0 || which > 6) return TPE_E_INVALID;
+  if (!h || !per_second || which < 0 || which > 7) return TPE_E_INVALID;
   CKH(hipSetDevice(h->device));
   hipDeviceProp_t prop;
   CKH(hipGetDeviceProperties(&prop, h->device));
@@ -1727,8 +1731,9 @@ int tpe_microbench(tpe_handle_t h, int32_t which, double *per_second) {
   dfree(sink);
   // results per thread-iteration: exp / FMA chains, erf chains, LSE pairs
   // (4 candidates x 8 components), quantized pairs (2 chains), shifted LSE
-  // pairs (4 x 8), block-local fp32 LSE pairs (4 x 8)
-  static const double per_iter[7] = {8.0, 16.0, 4.0, 32.0, 2.0, 32.0, 32.0};
+  // pairs (4 x 8), block-local fp32 LSE pairs (4 x 8), the fp32 per-group-lift
+  // pairs (4 x 8)
+  static const double per_iter[8] = {8.0, 16.0, 4.0, 32.0, 2.0, 32.0, 32.0, 32.0};
   *per_second = 4.0 * blocks * 256.0 * iters * per_iter[which] / (ms * 1e-3);
   return TPE_OK;
 }

@@ -82,9 +82,10 @@ struct MixInfo {
 // terms of a K-component mixture move the lpdf by at most K * 2^-D <=
 // 2^-kLseDeadBase ~ 1e-9 relative -- 1000x inside the 1e-6 parity bar.
 constexpr float kLseDeadBase = 30.0f;
-// census counters (tpe_plan_census): quantized total / live / evaluated,
-// log-sum-exp total / (reserved) / evaluated
-constexpr int kCensus = 6;
+// census counters (tpe_plan_census_n): quantized total / live / evaluated,
+// log-sum-exp total / one-exponent evaluated / evaluated / evaluated in the
+// block-local fp32 per-group-lift form
+constexpr int kCensus = 7;
 
 // Per-component scoring coefficients (make_coef, tpe_device.hpp), 4 fields:
 //   LSE: x = alpha, y = beta, z = gamma (t = alpha + y'(beta + gamma y'))

@@ -577,6 +577,62 @@ __global__ __launch_bounds__(256) void k_micro(int iters, double *sink) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) acc += sm[c];
     if (acc == 12345.0) sink[t] = acc;
+  } else if constexpr (WHICH == 7) {
+    // one log-sum-exp pair of mode 3's per-group-lift loop (lse_terms_z /
+    // lse_fold_z): z = t - A by packed fp32 FMAs, fp32 group max, the fp64
+    // integer lift, exp2 of z + (A - m), fp32 tree, fp64 sum; 4 x 8
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    double y[4], sm[4], m[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) { y[c] = 1e-3 * (t + c); sm[c] = 0.0; m[c] = -INFINITY; }
+    float ca[8], cb[8], cc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { ca[k] = -0.1f * k; cb[k] = 0.01f * k; cc[k] = -0.5f - 0.01f * k; }
+    const double centre = 0.25;
+    float A = 3.0f;
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float u = (float)(y[c] - centre);
+        const f2v u2 = {u, u};
+        float z[8];
+#pragma unroll
+        for (int k = 0; k < 8; k += 2) {
+          const f2v a2 = {ca[k], ca[k + 1]}, b2 = {cb[k], cb[k + 1]}, c2 = {cc[k], cc[k + 1]};
+          const f2v zz = __builtin_elementwise_fma(__builtin_elementwise_fma(c2, u2, b2), u2, a2);
+          z[k] = zz.x;
+          z[k + 1] = zz.y;
+        }
+        float mx[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) mx[k] = z[k];
+#pragma unroll
+        for (int w = 4; w > 0; w >>= 1)
+#pragma unroll
+          for (int k = 0; k < w; ++k) mx[k] = fmaxf(mx[k], mx[k + w]);
+        const double mn = fmax(m[c], (double)A + (double)ceilf(mx[0]));
+        sm[c] = ldexp(sm[c], (int)fmax(m[c] - mn, -2100.0));
+        m[c] = mn;
+        const float off = (float)((double)A - mn);
+        const f2v o2 = {off, off};
+        float e[8];
+#pragma unroll
+        for (int k = 0; k < 8; k += 2) {
+          const f2v zz = f2v{z[k], z[k + 1]} + o2;
+          e[k] = __builtin_amdgcn_exp2f(zz.x);
+          e[k + 1] = __builtin_amdgcn_exp2f(zz.y);
+        }
+        const float t0 = (e[0] + e[2]) + (e[1] + e[3]);
+        const float t1 = (e[4] + e[6]) + (e[5] + e[7]);
+        sm[c] += (double)(t0 + t1);
+        y[c] += 1e-9;
+      }
+      A += 1e-7f;
+    }
+    double acc = 0.0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc += sm[c] + m[c];
+    if (acc == 12345.0) sink[t] = acc;
   } else if constexpr (WHICH == 4) {
     // one quantized pair exactly as k_score computes a live one: two OCML
     // fp64 erf, the reference's Phi and two-stage increment; 2 chains
@@ -622,6 +678,7 @@ hipError_t launch_micro(int which, int blocks, int iters, double *sink, hipStrea
     case 4: k_micro<4><<<blocks, 256, 0, st>>>(iters, sink); break;
     case 5: k_micro<5><<<blocks, 256, 0, st>>>(iters, sink); break;
     case 6: k_micro<6><<<blocks, 256, 0, st>>>(iters, sink); break;
+    case 7: k_micro<7><<<blocks, 256, 0, st>>>(iters, sink); break;
     default: k_micro<2><<<blocks, 256, 0, st>>>(iters, sink); break;
   }
   return hipGetLastError();

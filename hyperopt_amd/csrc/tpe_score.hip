@@ -200,6 +200,7 @@ struct LseWindow {
 // the ones in evaluated (not skipped) blocks.
 struct LseCensus {
   uint32_t total, exec, shift;  // shift: the evaluated ones in the one-exponent form
+  uint32_t f32;                 // the evaluated ones in the fp32 per-group-lift form
 };
 
 // A block's envelope bound over the wave's candidate range [lo, hi]: the
@@ -215,11 +216,67 @@ __device__ __forceinline__ float envelope_bound(const float4 e, const LseWindow 
 // their envelopes, tpe_internal.hpp kLseDeadBase), a ballot gives the round's
 // live blocks, and only those are evaluated, in the same order as the full
 // loop.  prune = false: every block is live.
-template <int KR, bool CENSUS, int STRIDE = kWaves>
+// The same fold from the block-local fp32 form (prune mode 3, Coef32, blocks
+// that are not wide): z = t - A by two packed fp32 FMAs per component pair
+// (lse_terms_z, before the next block's coefficients are loaded), then the
+// group max in fp32, the integer lift m = max(m, A + ceil(max z)) in fp64 as
+// before, and 2^(z + (A - m)) with A - m an exact integer (lse_fold_z).
+template <int KR>
+__device__ __forceinline__ void lse_terms_z(const CoefGroup32 &g, const double (&y)[KR],
+                                            float (&z)[KR][kGroup]) {
+#pragma unroll
+  for (int r = 0; r < KR; ++r) {
+    const float u = (float)(y[r] - g.m);
+    const f2v u2 = {u, u};
+#pragma unroll
+    for (int j = 0; j < kGroup; j += 2) {
+      const f2v a2 = {g.a[j], g.a[j + 1]}, b2 = {g.b[j], g.b[j + 1]}, c2 = {g.c[j], g.c[j + 1]};
+      const f2v t = __builtin_elementwise_fma(__builtin_elementwise_fma(c2, u2, b2), u2, a2);
+      z[r][j] = t.x;
+      z[r][j + 1] = t.y;
+    }
+  }
+}
+template <int KR>
+__device__ __forceinline__ void lse_fold_z(const float (&z)[KR][kGroup], float A, double (&m)[KR],
+                                           double (&s)[KR]) {
+#pragma unroll
+  for (int r = 0; r < KR; ++r) {
+    float mx[kGroup];
+#pragma unroll
+    for (int j = 0; j < kGroup; ++j) mx[j] = z[r][j];
+#pragma unroll
+    for (int w = kGroup / 2; w > 0; w >>= 1)
+#pragma unroll
+      for (int j = 0; j < w; ++j) mx[j] = fmaxf(mx[j], mx[j + w]);
+    const double mn = fmax(m[r], (double)A + (double)ceilf(mx[0]));
+    s[r] = ldexp(s[r], (int)fmax(m[r] - mn, -2100.0));
+    m[r] = mn;
+    const double ms = mn == -INFINITY ? 0.0 : mn;
+    const float off = (float)((double)A - ms);
+    const f2v o2 = {off, off};
+    float e[kGroup];
+#pragma unroll
+    for (int j = 0; j < kGroup; j += 2) {
+      const f2v zz = f2v{z[r][j], z[r][j + 1]} + o2;
+      e[j] = __builtin_amdgcn_exp2f(zz.x);
+      e[j + 1] = __builtin_amdgcn_exp2f(zz.y);
+    }
+    const float t0 = (e[0] + e[2]) + (e[1] + e[3]);
+    const float t1 = (e[4] + e[6]) + (e[5] + e[7]);
+    s[r] += (double)(t0 + t1);
+  }
+}
+
+// F32 (prune mode 3): blocks that are not wide take lse_terms_z / lse_fold_z in the
+// pipelined loop, wide ones (the sign of their envelope's a^2) the fp64 fold
+// in a second loop after each round.
+template <int KR, bool CENSUS, int STRIDE = kWaves, bool F32 = false>
 __device__ __forceinline__ void lse_chunks(KDbl *__restrict__ cs, const Coef *__restrict__ cv,
                                            int c0, int nb, const double (&y)[KR],
                                            LseAcc (&out)[KR], bool prune, LseWindow win,
-                                           int nvalid, LseCensus &cen) {
+                                           int nvalid, LseCensus &cen,
+                                           KC32 *__restrict__ c32 = nullptr) {
   const int lane = threadIdx.x & 63;
   double m[KR], s[KR], y2[KR];
 #pragma unroll
@@ -229,14 +286,16 @@ __device__ __forceinline__ void lse_chunks(KDbl *__restrict__ cs, const Coef *__
     const int c = r0 + STRIDE * lane;
     const int k0 = c * kChunk;
     const bool has0 = c < nch, has1 = has0 && k0 + kGroup < nb;
-    bool live0 = has0, live1 = has1;
-    if (prune && has0) {
+    bool live0 = has0, live1 = has1, wide0 = false, wide1 = false;
+    if ((prune || F32) && has0) {
       const double *t = reinterpret_cast<const double *>(cv);
       const float4 e0 = *reinterpret_cast<const float4 *>(t + coef_off(k0, 3));
-      live0 = envelope_bound(e0, win) >= win.thr;
+      if (prune) live0 = envelope_bound(e0, win) >= win.thr;
+      wide0 = __builtin_signbit(e0.w);
       if (has1) {
         const float4 e1 = *reinterpret_cast<const float4 *>(t + coef_off(k0 + kGroup, 3));
-        live1 = envelope_bound(e1, win) >= win.thr;
+        if (prune) live1 = envelope_bound(e1, win) >= win.thr;
+        wide1 = __builtin_signbit(e1.w);
       }
     }
     if constexpr (CENSUS) {
@@ -249,8 +308,14 @@ __device__ __forceinline__ void lse_chunks(KDbl *__restrict__ cs, const Coef *__
       }
       cen.total += tot * (uint32_t)nvalid;
       cen.exec += ex * (uint32_t)nvalid;
+      if constexpr (F32) {
+        uint32_t fx = (uint32_t)((live0 && !wide0 ? n0 : 0) + (live1 && !wide1 ? n1 : 0));
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) fx += __shfl_xor(fx, o, 64);
+        cen.f32 += fx * (uint32_t)nvalid;
+      }
     }
-    uint64_t m0 = __ballot(live0), m1 = __ballot(live1);
+    uint64_t m0 = __ballot(live0 && !(F32 && wide0)), m1 = __ballot(live1 && !(F32 && wide1));
     // live blocks in order: chunk j's block 0 before its block 1 before chunk
     // j + 1 (the padding components of a last block have alpha = -inf,
     // make_coef_pad, so no tail masking is needed)
@@ -260,15 +325,37 @@ __device__ __forceinline__ void lse_chunks(KDbl *__restrict__ cs, const Coef *__
     // order, so only one batch may be in flight)
     int kg = 0;
     bool have = next_live<STRIDE>(m0, m1, r0, kg);
-    CoefGroup cgp;
-    if (have) load_group(cs, kg, cgp);
-    while (have) {
-      double t[KR][kGroup];
-      lse_terms<KR>(cgp, y, y2, t);
-      have = next_live<STRIDE>(m0, m1, r0, kg);  // (kg kept after the last)
-      load_group(cs, kg, cgp);  // unconditional: no branch merge of the registers
-      __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of the fold
-      lse_fold<KR>(t, m, s);
+    if constexpr (F32) {
+      CoefGroup32 g32;
+      if (have) load_group32(c32, kg, g32);
+      while (have) {
+        float z[KR][kGroup];
+        lse_terms_z<KR>(g32, y, z);
+        const float A = g32.A;
+        have = next_live<STRIDE>(m0, m1, r0, kg);
+        load_group32(c32, kg, g32);
+        __builtin_amdgcn_sched_barrier(0);
+        lse_fold_z<KR>(z, A, m, s);
+      }
+      uint64_t x0 = __ballot(live0 && wide0), x1 = __ballot(live1 && wide1);
+      while (next_live<STRIDE>(x0, x1, r0, kg)) {
+        CoefGroup g;
+        load_group(cs, kg, g);
+        double t[KR][kGroup];
+        lse_terms<KR>(g, y, y2, t);
+        lse_fold<KR>(t, m, s);
+      }
+    } else {
+      CoefGroup cgp;
+      if (have) load_group(cs, kg, cgp);
+      while (have) {
+        double t[KR][kGroup];
+        lse_terms<KR>(cgp, y, y2, t);
+        have = next_live<STRIDE>(m0, m1, r0, kg);  // (kg kept after the last)
+        load_group(cs, kg, cgp);  // unconditional: no branch merge of the registers
+        __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of the fold
+        lse_fold<KR>(t, m, s);
+      }
     }
   }
 #pragma unroll
@@ -786,7 +873,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
     // wave index as a scalar: the component addresses below are wave-uniform,
     // so the coefficients come in through scalar loads (SGPR operands)
     const int wv = __builtin_amdgcn_readfirstlane(wave);
-    LseCensus lcen{0u, 0u, 0u};
+    LseCensus lcen{0u, 0u, 0u, 0u};
     int nvalid = 0;
 #pragma unroll
     for (int r = 0; r < KR; ++r) nvalid += valid[r] ? 1 : 0;
@@ -827,8 +914,13 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
             // ~3 live blocks per pass.  Nothing compares the two tile shapes
             // bit for bit: batched, sharded and chunked runs of one draw take
             // the same tile shape.)
-            lse_chunks<KR, CENSUS, 1>(uniform_ptr(cm), cm, 0, K, y, lacc[mix], prune, win, nvalid,
-                                      lcen);
+            if (A.lse_prune > 2)  // block-local fp32 (Coef32) for the blocks that allow it
+              lse_chunks<KR, CENSUS, 1, true>(
+                  uniform_ptr(cm), cm, 0, K, y, lacc[mix], prune, win, nvalid, lcen,
+                  uniform_ptr32(A.coef32 + (mix ? sa : sb) * (A.kcap / kCoefBlock)));
+            else
+              lse_chunks<KR, CENSUS, 1>(uniform_ptr(cm), cm, 0, K, y, lacc[mix], prune, win,
+                                        nvalid, lcen);
           } else {
             lse_chunks<KR, CENSUS, kWaves>(uniform_ptr(cm), cm, wv, K, y, lacc[mix], prune, win,
                                            nvalid, lcen);
@@ -857,9 +949,9 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
     }
     if constexpr (CENSUS && LSE) {
       // nvalid is per lane: the per-lane sums add up to the wave's pairs
-      unsigned long long c2[3] = {lcen.total, lcen.exec, lcen.shift};
+      unsigned long long c2[4] = {lcen.total, lcen.exec, lcen.shift, lcen.f32};
 #pragma unroll
-      for (int q = 0; q < 3; ++q) {
+      for (int q = 0; q < 4; ++q) {
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) c2[q] += __shfl_xor(c2[q], o, 64);
       }
@@ -867,6 +959,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
         atomicAdd(A.census + 3, c2[0]);
         atomicAdd(A.census + 4, c2[2]);
         atomicAdd(A.census + 5, c2[1]);
+        atomicAdd(A.census + 6, c2[3]);
       }
     }
     if constexpr (!WT) {

@@ -276,6 +276,10 @@ int tpe_plan_set_lattice(tpe_plan_t p, int32_t enable);
  * zeros; a wave's retried pass counts again) -- and switch the census on (enable != 0)
  * or off for the following suggests.  counts has 6 entries.               */
 int tpe_plan_census(tpe_plan_t p, int32_t enable, int64_t *counts);
+/* The same with n_counts entries (up to 7): [6] of [5] the log-sum-exp pairs
+ * evaluated in the block-local fp32 per-group-lift form (prune mode 3 on
+ * mixtures below the one-exponent size).                                   */
+int tpe_plan_census_n(tpe_plan_t p, int32_t enable, int64_t *counts, int32_t n_counts);
 
 /* Prior draws of n_suggest whole suggestions (rand.suggest, the TPE startup
  * phase: hyperopt/rand.py:14-33, pyll/stochastic.py:30-142): every active hp
@@ -304,7 +308,8 @@ int tpe_plan_set_prune(tpe_plan_t p, int32_t mode);
  * log-sum-exp (candidate, component) pair of the scoring kernel (pairs/s),
  * 4 a live quantized pair (2 fp64 erf; pairs/s), 5 the log-sum-exp pair of
  * the one-exponent-per-wave loop (tpe_plan_set_prune mode 2; pairs/s), 6 the
- * same pair in block-local fp32 (mode 3; pairs/s).                          */
+ * same pair in block-local fp32 (mode 3; pairs/s), 7 the per-group-lift pair
+ * in block-local fp32 (mode 3 below the one-exponent size; pairs/s).        */
 int tpe_microbench(tpe_handle_t h, int32_t which, double *per_second);
 
 #ifdef __cplusplus

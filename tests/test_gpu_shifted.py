@@ -221,6 +221,50 @@ def test_shifted_form_every_lse_kind_vs_oracle(lse_plan):
                     below=_delta(lb, ref['llik_b']), above=_delta(la, ref['llik_a']))
 
 
+def test_exact_wave_loop_every_lse_kind_vs_oracle():
+    """Mixtures below lse_shift_min (K ~ 1.5e3: config 3's branches, config
+    5's K_a = 993) keep the per-group-lift loop on the bucketed wave tiles;
+    in mode 3 its non-wide blocks run from the block-local fp32 table
+    (lse_terms_z / lse_fold_z).  Every kind against the oracle, modes 1 and
+    3 (the census shows no one-exponent pairs)."""
+    dom = Domain(lambda x: 0.0, _lse_space())
+    L, vals, act = _lse_history(dom, n=1500)
+    hps, conds, pprior = dom.space.engine_tables()
+    plan = E.Plan(E.default_engine(), hps, conds, pprior, max_trials=L.size)
+    plan.set_history(L, vals, act)
+    plan.fit()
+    obs = _oracle_obs(dom, L, vals, act)
+    tabs = dom.space.engine_tables()[0]
+    rs = np.random.RandomState(4)
+    for h in dom.space.hps:
+        i = h.index
+        assert 1000 < plan.mixture(i, 1)[0].size < 2048
+        t = tabs[i]
+        w, mu, sg = plan.mixture(i, 0)
+        lo = t.low if t.flags & E.HAS_LOW else None
+        hi = t.high if t.flags & E.HAS_HIGH else None
+        x = plan.engine.sample(t.family, w, mu, sg, lo, hi, None, seed=98, stream=i, n=8192)
+        wide = rs.uniform(t.prior_mu - 2.5 * t.prior_sigma, t.prior_mu + 2.5 * t.prior_sigma, 4096)
+        if t.family == E.LGMM:
+            wide = np.exp(wide)
+        if lo is not None:
+            wide = np.clip(wide, math.exp(lo) if t.family == E.LGMM else lo,
+                           math.exp(hi) if t.family == E.LGMM else hi)
+        x = np.concatenate([x, wide])
+        ref = _oracle_score(dom, obs, h.label, x)
+        for mode in (1, 3):
+            plan.census(True)
+            lb, la, bi, bs = plan.score_candidates(i, x, sorted_mode=mode)
+            census = plan.census(False)
+            assert_close(lb, ref['llik_b'], msg='%s below, mode %d' % (h.label, mode))
+            assert_close(la, ref['llik_a'], msg='%s above, mode %d' % (h.label, mode))
+            with np.errstate(all='ignore'):
+                assert argmax_equiv(ref['llik_b'] - ref['llik_a'], bi), (h.label, mode)
+            assert census[4] == 0, census
+            _record('exact_%s_mode%d' % (h.label, mode), census=list(census),
+                    below=_delta(lb, ref['llik_b']), above=_delta(la, ref['llik_a']))
+
+
 def test_shifted_form_clustered_history_vs_oracle():
     """A history of tight clusters with wide gaps (K_a ~ 1e4, sigmas at the
     prior_sigma / 100 floor): the coefficient blocks that straddle a gap put
