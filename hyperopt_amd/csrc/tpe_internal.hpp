@@ -48,9 +48,14 @@ __host__ __device__ constexpr int tile_rows(int kind) {
              ? 1
          : (kind == KIND_CAT || kind == KIND_LAT) ? 4 : 2;
 }
-// waves of a block holding their own candidates (wave tiles), else 1
+// waves of a block holding their own candidates (wave tiles), else 1 (the
+// block's waves split the components of the same candidates).  The lookup
+// kinds (categorical, value lattice) have no components to split: every wave
+// takes its own 256 candidates (one-wave tiles left 7 of 8 waves idle, and
+// a 1e6-candidate slot 3906 blocks instead of 489).
 __host__ __device__ constexpr int tile_waves(int kind) {
-  return (kind == KIND_LSE_GW || kind == KIND_LSE_LW) ? 8 : 1;
+  return (kind == KIND_LSE_GW || kind == KIND_LSE_LW || kind == KIND_CAT || kind == KIND_LAT) ? 8
+                                                                                             : 1;
 }
 // candidates of one scoring block of the kind
 __host__ __device__ constexpr int tile_cands(int kind) {
