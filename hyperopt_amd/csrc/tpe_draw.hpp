@@ -185,12 +185,55 @@ __device__ void build_table(const tpe_hp &H, int K, const double *__restrict__ w
   block_inclusive_scan(T.cdf, K, T.wtot);
 }
 
+// erfcinv(y) for y in (0, 1] (the tail-side inverse CDF of the table
+// sampler; the value a sample takes, so ~4e-7 relative on the normal
+// quantile is immaterial): Giles' single-precision erfinv polynomials
+// ("Approximating the erfinv function", GPU Computing Gems, 2011) in
+// w = -log(y (2 - y)), with w from the fp64 y by frexp + v_log_f32 (no
+// cancellation in 1 - x, full range of y), both branches evaluated without
+// divergence; beyond w = 36 (y < ~1e-16, outside the fitted range) the fp64
+// OCML erfcinv.
+__device__ __forceinline__ double erfcinv_fast(double y) {
+  int e1, e2;
+  const double m1 = frexp(y, &e1), m2 = frexp(2.0 - y, &e2);
+  const float l2 = __builtin_amdgcn_logf((float)m1) + __builtin_amdgcn_logf((float)m2) +
+                   (float)(e1 + e2);                   // log2(y (2 - y))
+  const float w = -0.6931471805599453f * l2;
+  if (!(w <= 36.0f)) return erfcinv(y);
+  const float wc = w - 2.5f;
+  float pc = 2.81022636e-08f;
+  pc = fmaf(pc, wc, 3.43273939e-07f);
+  pc = fmaf(pc, wc, -3.5233877e-06f);
+  pc = fmaf(pc, wc, -4.39150654e-06f);
+  pc = fmaf(pc, wc, 0.00021858087f);
+  pc = fmaf(pc, wc, -0.00125372503f);
+  pc = fmaf(pc, wc, -0.00417768164f);
+  pc = fmaf(pc, wc, 0.246640727f);
+  pc = fmaf(pc, wc, 1.50140941f);
+  const float wt = __builtin_sqrtf(w) - 3.0f;
+  float pt = -0.000200214257f;
+  pt = fmaf(pt, wt, 0.000100950558f);
+  pt = fmaf(pt, wt, 0.00134934322f);
+  pt = fmaf(pt, wt, -0.00367342844f);
+  pt = fmaf(pt, wt, 0.00573950773f);
+  pt = fmaf(pt, wt, -0.0076224613f);
+  pt = fmaf(pt, wt, 0.00943887047f);
+  pt = fmaf(pt, wt, 1.00167406f);
+  pt = fmaf(pt, wt, 2.83297682f);
+  const double p = (double)(w < 5.0f ? pc : pt);
+  return p * (1.0 - y);
+}
+
 template <int CAP>
 __device__ double draw_table(const tpe_hp &H, int K, const double *__restrict__ mu,
                              const double *__restrict__ sg, const DrawTableT<CAP> &T,
                              uint64_t seed, uint64_t gi, uint32_t stream) {
-  const Draw d = draw4(seed, gi, stream, 0);
-  const int k = pick_cdf(T.cdf, K, d.u0);
+  // (the words of draw4's first Philox block: u0 picks, u1 inverts; the
+  // second block -- u2 -- only for the unbounded Box-Muller)
+  const U4 c0{(uint32_t)gi, (uint32_t)(gi >> 32), stream, 0u};
+  const U4 r0 = philox(c0, (uint32_t)seed, (uint32_t)(seed >> 32));
+  const double u0 = u53(r0.x, r0.y), u1 = u53(r0.z, r0.w);
+  const int k = pick_cdf(T.cdf, K, u0);
   if (H.family == TPE_CAT) return (double)k;
   double x;
   if (H.flags & (TPE_HAS_LOW | TPE_HAS_HIGH)) {
@@ -198,17 +241,20 @@ __device__ double draw_table(const tpe_hp &H, int K, const double *__restrict__ 
     const double s2 = 1.4142135623730951 * sg[k], b = T.base[k], m = T.mass[k];
     const int md = T.mode[k];
     double q, side;
-    if (md == 1) { q = b - d.u1 * m; side = 1.0; }        // upper tail Q
+    if (md == 1) { q = b - u1 * m; side = 1.0; }          // upper tail Q
     else {
-      const double pp = b + d.u1 * m;                      // Phi
+      const double pp = b + u1 * m;                        // Phi
       if (md == 2 || pp < 0.5) { q = pp; side = -1.0; }
       else { q = 1.0 - pp; side = 1.0; }
     }
-    x = mu[k] + side * s2 * erfcinv(2.0 * q);
+    x = mu[k] + side * s2 * erfcinv_fast(2.0 * q);
     if (!(x >= H.low)) x = H.low;  // rounding at the bounds / zero-mass picks
     if (!(x < H.high)) x = nextafter(H.high, -INFINITY);
   } else {
-    x = mu[k] + sg[k] * (sqrt(-2.0 * log(1.0 - d.u1)) * cospi(2.0 * d.u2));
+    const U4 c1{(uint32_t)gi, (uint32_t)(gi >> 32), stream, 1u};
+    const U4 r1 = philox(c1, (uint32_t)seed, (uint32_t)(seed >> 32));
+    const double u2 = u53(r1.x, r1.y);
+    x = mu[k] + sg[k] * (sqrt(-2.0 * log(1.0 - u1)) * cospi(2.0 * u2));
   }
   if (H.family == TPE_LGMM) x = exp(x);
   if (H.flags & TPE_HAS_Q) x = rint(x / H.q) * H.q;
