@@ -19,80 +19,6 @@ namespace tpe {
 
 constexpr int kSortMax = 8192;  // candidates per bucketing chunk
 
-// Stable counting scatter by an 8-bit bucket: element i of [0, n) goes to
-// position dest(i) = (elements of lower buckets) + (elements of its bucket
-// with a lower index), independent of thread timing (an atomic-increment
-// scatter orders a bucket's elements by arrival, so which scoring tile a
-// candidate lands in -- and the log-sum-exp block skip of that tile --
-// would vary from run to run).  Wave w takes elements [w * per, ...) in
-// order; per (wave, bucket) counts from 8-ballot lane matching, one scan
-// over (bucket, wave), then the same walk writes the destinations.
-// cnt: NW * 256 ints of LDS; every thread of the block calls it.
-__device__ __forceinline__ uint64_t lanes_equal8(uint32_t d, bool v) {
-  uint64_t m = __ballot(v);
-#pragma unroll
-  for (int b = 0; b < 8; ++b) {
-    const bool x = (d >> b) & 1u;
-    const uint64_t bb = __ballot(x);
-    m &= x ? bb : ~bb;
-  }
-  return m;
-}
-
-template <int NW, typename Dest>
-__device__ __forceinline__ void stable_bucket_scatter(const unsigned char *bk, int n, int *cnt,
-                                                      Dest dest) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int per = ((n + NW * 64 - 1) / (NW * 64)) * 64;
-  const int r0 = w * per, r1 = min(n, r0 + per);
-  int *mine = cnt + w * 256;
-  for (int b = lane; b < 256; b += 64) mine[b] = 0;
-  // (a wave's LDS ops complete in order: no barrier between its own rows)
-  for (int base = r0; base < r1; base += 64) {
-    const int i = base + lane;
-    const bool v = i < r1;
-    const uint32_t d = v ? bk[i] : 0u;
-    const uint64_t mt = lanes_equal8(d, v);
-    if (v && lane == __ffsll((long long)mt) - 1) mine[d] += __popcll(mt);
-  }
-  __syncthreads();
-  // bucket b (thread b of the first 256): its total over the waves, a block
-  // scan of the totals, then the (bucket, wave) bases in place
-  static_assert(NW * 64 >= 256, "one thread per bucket");
-  __shared__ int wtot[4];
-  int tot = 0;
-  if (threadIdx.x < 256)
-    for (int q = 0; q < NW; ++q) tot += cnt[q * 256 + threadIdx.x];
-  int x = tot;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63 && w < 4) wtot[w] = x;
-  __syncthreads();
-  if (threadIdx.x < 256) {
-    int acc = x - tot;
-    for (int q = 0; q < w; ++q) acc += wtot[q];
-    for (int q = 0; q < NW; ++q) {
-      const int c = cnt[q * 256 + threadIdx.x];
-      cnt[q * 256 + threadIdx.x] = acc;
-      acc += c;
-    }
-  }
-  __syncthreads();
-  for (int base = r0; base < r1; base += 64) {
-    const int i = base + lane;
-    const bool v = i < r1;
-    const uint32_t d = v ? bk[i] : 0u;
-    const uint64_t mt = lanes_equal8(d, v);
-    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    if (v) dest(i, mine[d] + __popcll(mt & lt));
-    if (v && lane == __ffsll((long long)mt) - 1) mine[d] += __popcll(mt);
-  }
-}
-
-
 // Candidate draws of one level (all its hps): grid = (blocks, hps of the
 // level, suggestions), one candidate per thread per step.  Counter = (global
 // candidate index, hp id, iteration), key = suggestion seed, so the
@@ -128,123 +54,39 @@ __global__ __launch_bounds__(kDrawThreads) void k_draw(ScoreArgs A) {
   }
 }
 
-// Large draws with value bucketing (the default above 4M draws): a block of
-// 256 threads draws kSortedBlock consecutive candidates of one (suggestion,
-// slot) -- 16 per thread -- and, for the per-candidate log-sum-exp and erf
-// kinds, writes them grouped into kSortBuckets equal-width value buckets of
-// the block's range (log scale for LGMM), with their chunk positions.  A
-// scoring tile (64 or 128 consecutive candidates) then spans a narrow value
-// range, so whole component blocks / chunks of a mixture are provably zero
-// for the wave and skipped (tpe_score.hip).  The candidate values are those
-// of the unsorted draw (counter = global index); only their order changes,
-// and the argmax tie-break uses the original index.
-constexpr int kSortBuckets = 256;
-
-// the scoring kind of a level slot (the groups are emitted heaviest kind
-// first, set_score_groups, not in slot order)
 __device__ __forceinline__ int slot_kind(const ScoreArgs &A, int slot) {
   for (int g = 0; g < A.n_groups; ++g)
     if (slot >= A.grp_slot0[g] && slot < A.grp_slot0[g] + A.grp_slots[g]) return A.grp_kind[g];
   return -1;
 }
 
-template <int CAP>
-struct SortedDrawLds {
-  DrawTableT<CAP> T;
-  double xs[kSortedBlock];          // the block's draws, in draw order
-  unsigned char bk[kSortedBlock];   // their buckets
-  int32_t cnt[kDrawThreads / 64 * kSortBuckets];  // stable scatter counts / bases
-  double red[2][kDrawThreads / 64];
-};
-
-// EXT (k_sort_ext): the block's values come from src[slot][n_cand] instead
-// of the draw (given candidates scored exactly as a large draw's are)
 template <int CAP, bool EXT>
 __device__ __forceinline__ void sorted_block(const ScoreArgs &A, int32_t *__restrict__ pos_out,
                                              const double *__restrict__ src,
-                                             SortedDrawLds<CAP> &L) {
+                                             SortedDrawLds<CAP, kDrawThreads> &L) {
   const int s = blockIdx.z;
   const int slot = row_slot(A, s, 0, A.n_slots, blockIdx.y);
   if (slot < 0) return;
   const int hp = A.level_hps[slot];
-  const tpe_hp H = A.hps[hp];
   if (!A.force_active && !A.compact &&
-      !hp_active(H, A.results + (int64_t)s * A.n_hp, A.cond_parent, A.cond_branch))
+      !hp_active(A.hps[hp], A.results + (int64_t)s * A.n_hp, A.cond_parent, A.cond_branch))
     return;
-  const int64_t sb = 2 * (int64_t)hp;
-  const double *bw = A.mw + sb * A.kcap, *bmu = A.mmu + sb * A.kcap, *bsg = A.msig + sb * A.kcap;
-  const int K = A.info[sb].K;
-  const bool tab = !EXT && K >= 1 && K <= CAP;
-  if constexpr (!EXT) {
-    if (tab) build_table(H, K, bw, bmu, bsg, L.T);
-  }
-  const uint64_t seed = suggestion_seed(A, s);
-  const int64_t base = (int64_t)blockIdx.x * kSortedBlock;
-  const int n = (int)min<int64_t>(kSortedBlock, A.n_cand - base);
-  const int64_t off = (int64_t)s * A.cand_sstride + (int64_t)slot * A.n_cand + base;
-  double *out = const_cast<double *>(A.cand) + off;
-  const int t = threadIdx.x;
   const int kind = slot_kind(A, slot);
-  const bool bucket = kind_lse(kind) || kind == KIND_ERF_G || kind == KIND_ERF_L;
-  const bool lg = kind_logn(kind);
-  double lo = INFINITY, hi = -INFINITY;
-#pragma unroll 1
-  for (int i = t; i < n; i += kDrawThreads) {
-    const uint64_t gi = (uint64_t)(A.cand_begin + base + i);
-    double x;
-    if constexpr (EXT) {
-      (void)gi; (void)seed; (void)bw;
-      x = src[(int64_t)slot * A.n_cand + base + i];
-    } else {
-      x = tab ? draw_table_ool<CAP>(A.hps + hp, K, bmu, bsg, &L.T, seed, gi, (uint32_t)hp)
-              : draw_one_ool(A.hps + hp, A.info + sb, bw, bmu, bsg, seed, gi, (uint32_t)hp);
-    }
-    if (!bucket) {
-      out[i] = x;
-      continue;
-    }
-    L.xs[i] = x;
-    const double key = lg ? log(x) : x;
-    if (fabs(key) < INFINITY) { lo = fmin(lo, key); hi = fmax(hi, key); }
-  }
-  if (!bucket) return;
-  // block range of the finite keys
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    lo = fmin(lo, __shfl_xor(lo, o, 64));
-    hi = fmax(hi, __shfl_xor(hi, o, 64));
-  }
-  const int lane = t & 63, wv = t >> 6;
-  if (lane == 0) { L.red[0][wv] = lo; L.red[1][wv] = hi; }
-  __syncthreads();
-  lo = INFINITY; hi = -INFINITY;
-#pragma unroll
-  for (int w = 0; w < kDrawThreads / 64; ++w) { lo = fmin(lo, L.red[0][w]); hi = fmax(hi, L.red[1][w]); }
-  const double scale = hi > lo ? (double)kSortBuckets / (hi - lo) : 0.0;
-  for (int i = t; i < n; i += kDrawThreads) {
-    const double key = lg ? log(L.xs[i]) : L.xs[i];
-    int b = kSortBuckets - 1;
-    if (fabs(key) < INFINITY) b = min(kSortBuckets - 1, max(0, (int)((key - lo) * scale)));
-    L.bk[i] = (unsigned char)b;
-  }
-  __syncthreads();
-  // scatter into the block's slice (32 KB + 16 KB, merged in L2), stable
-  int32_t *po = pos_out + off;
-  stable_bucket_scatter<kDrawThreads / 64>(L.bk, n, L.cnt, [&](int i, int p) {
-    out[p] = L.xs[i];
-    po[p] = (int32_t)(base + i);
-  });
+  sorted_block_body<CAP, kDrawThreads, EXT>(
+      A, slot, s, (int64_t)blockIdx.x * kSortedBlock,
+      kind_lse(kind) || kind == KIND_ERF_G || kind == KIND_ERF_L, kind_logn(kind), pos_out, src,
+      L);
 }
 
 template <int CAP>
 __global__ __launch_bounds__(kDrawThreads) void k_draw_sorted(ScoreArgs A, int32_t *__restrict__ pos_out) {
-  __shared__ SortedDrawLds<CAP> L;
+  __shared__ SortedDrawLds<CAP, kDrawThreads> L;
   sorted_block<CAP, false>(A, pos_out, nullptr, L);
 }
 
 __global__ __launch_bounds__(kDrawThreads) void k_sort_ext(ScoreArgs A, const double *__restrict__ src,
                                                            int32_t *__restrict__ pos_out) {
-  __shared__ SortedDrawLds<1> L;
+  __shared__ SortedDrawLds<1, kDrawThreads> L;
   sorted_block<1, true>(A, pos_out, src, L);
 }
 
