@@ -921,6 +921,10 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
             else
               lse_chunks<KR, CENSUS, 1>(uniform_ptr(cm), cm, 0, K, y, lacc[mix], prune, win,
                                         nvalid, lcen);
+          } else if (A.lse_prune > 2) {
+            lse_chunks<KR, CENSUS, kWaves, true>(
+                uniform_ptr(cm), cm, wv, K, y, lacc[mix], prune, win, nvalid, lcen,
+                uniform_ptr32(A.coef32 + (mix ? sa : sb) * (A.kcap / kCoefBlock)));
           } else {
             lse_chunks<KR, CENSUS, kWaves>(uniform_ptr(cm), cm, wv, K, y, lacc[mix], prune, win,
                                            nvalid, lcen);
