@@ -310,64 +310,116 @@ __device__ __forceinline__ void wave_bitonic64_packed(uint64_t &k) {
   bitonic_stage<64, 4>(k); bitonic_stage<64, 2>(k); bitonic_stage<64, 1>(k);
 }
 
-__device__ __forceinline__ bool merge_sort_1024_packed(const uint64_t *keys, int n, int shift, bool lossy,
-                                       uint16_t *out, uint64_t *b0, uint64_t *b1) {
+// PER elements per thread (element e = u * 1024 + t for register u): PER = 1
+// sorts up to 1024 elements in two 4-way merge levels, PER = 4 up to 4096 in
+// three (the large-history fit's observation sides of 1k-4k trials, which the
+// 8-bit LSD radix sort took 8 passes of ~4 us over).  After the in-register
+// 64-runs the merge levels keep the 32 key bits (kb) and the positions (pb)
+// in separate LDS arrays and search only kb: every run of a quad holds a
+// contiguous position range, ascending with the run index, so an equal key of
+// an earlier run precedes the element and one of a later run follows it --
+// the searches read 4-byte words, half the LDS traffic of the packed words.
+template <int PER>
+__device__ __forceinline__ bool merge_sort_packed(const uint64_t *keys, int n, int shift, bool lossy,
+                                                  uint16_t *out, uint32_t *kb0, uint32_t *kb1,
+                                                  uint16_t *pb0, uint16_t *pb1) {
   const int t = threadIdx.x;
-  // padding (t >= n): all-ones key bits, position t > every real position
-  uint64_t k = (t < n ? ((keys[t] >> shift) << 32) : 0xFFFFFFFF00000000ull) | (uint64_t)t;
-  wave_bitonic64_packed(k);
-  b0[t] = k;
+  constexpr int kN = PER * kFitThreads;
+  uint32_t k[PER], p[PER];
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    k[u] = ~0u;
+    p[u] = 0u;
+    if (u * kFitThreads >= n) continue;  // all padding: never read (below)
+    const int e = u * kFitThreads + t;
+    // padding (e >= n): all-ones key bits, position e > every real position
+    uint64_t w = (e < n ? ((keys[e] >> shift) << 32) : 0xFFFFFFFF00000000ull) | (uint64_t)e;
+    wave_bitonic64_packed(w);
+    k[u] = (uint32_t)(w >> 32);
+    p[u] = (uint32_t)w;
+    kb0[e] = k[u];
+    pb0[e] = (uint16_t)p[u];
+  }
   __syncthreads();
-  // two 4-way merge levels (64 -> 256 -> 1024): an element's position in its
-  // quad of runs is its index in its own run plus its rank in each of the
-  // three others (all words distinct), three branch-free binary searches
-  // side by side -- half the dependent LDS reads of four pairwise levels
+  // 4-way merge levels (64 -> 256 -> 1024 [-> 4096]): an element's position in
+  // its quad of runs is its index in its own run plus its rank in each of the
+  // three others, three branch-free binary searches side by side -- half the
+  // dependent LDS reads of pairwise levels
   static_assert(kFitThreads == 1024, "64 * 4 * 4");
-  uint64_t *sk = b0, *dk = b1;
+  uint32_t *sk = kb0, *dk = kb1;
+  uint16_t *sp = pb0, *dp = pb1;
 #pragma unroll
-  for (int len = 64; len < kFitThreads; len <<= 2) {
-    const int qb = t & ~(4 * len - 1), r = (t / len) & 3;
-    const uint64_t *o1 = sk + qb + ((r + 1) & 3) * len, *o2 = sk + qb + ((r + 2) & 3) * len,
-                   *o3 = sk + qb + ((r + 3) & 3) * len;
-    int i1 = 0, i2 = 0, i3 = 0;
+  for (int len = 64; len < kN; len <<= 2) {
 #pragma unroll
-    for (int step = len / 2; step > 0; step >>= 1) {
-      i1 += (o1[i1 + step - 1] < k) ? step : 0;
-      i2 += (o2[i2 + step - 1] < k) ? step : 0;
-      i3 += (o3[i3 + step - 1] < k) ? step : 0;
+    for (int u = 0; u < PER; ++u) {
+      if (u * kFitThreads >= n) continue;  // (block-uniform)
+      const int e = u * kFitThreads + t;
+      const int qb = e & ~(4 * len - 1), r = (e / len) & 3;  // (r: wave-uniform)
+      const int j1 = (r + 1) & 3, j2 = (r + 2) & 3, j3 = (r + 3) & 3;
+      const uint32_t *o1 = sk + qb + j1 * len, *o2 = sk + qb + j2 * len, *o3 = sk + qb + j3 * len;
+      // count o[i] < key, plus o[i] == key in an earlier run: o[i] < key + (j < r)
+      const uint64_t x1 = (uint64_t)k[u] + (j1 < r ? 1u : 0u), x2 = (uint64_t)k[u] + (j2 < r ? 1u : 0u),
+                     x3 = (uint64_t)k[u] + (j3 < r ? 1u : 0u);
+      // a run that is all padding (first position >= n, all keys all-ones)
+      // is not searched: an element of a later run (padding too) ranks after
+      // all of it, any other after none of it (runs of a skipped u hold no
+      // data, and are only ever such runs)
+      const bool s1 = qb + j1 * len < n, s2 = qb + j2 * len < n, s3 = qb + j3 * len < n;
+      int i1 = 0, i2 = 0, i3 = 0;
+#pragma unroll
+      for (int step = len / 2; step > 0; step >>= 1) {
+        if (s1) i1 += ((uint64_t)o1[i1 + step - 1] < x1) ? step : 0;
+        if (s2) i2 += ((uint64_t)o2[i2 + step - 1] < x2) ? step : 0;
+        if (s3) i3 += ((uint64_t)o3[i3 + step - 1] < x3) ? step : 0;
+      }
+      i1 = s1 ? i1 + (((uint64_t)o1[i1] < x1) ? 1 : 0) : (j1 < r ? len : 0);
+      i2 = s2 ? i2 + (((uint64_t)o2[i2] < x2) ? 1 : 0) : (j2 < r ? len : 0);
+      i3 = s3 ? i3 + (((uint64_t)o3[i3] < x3) ? 1 : 0) : (j3 < r ? len : 0);
+      const int dst = qb + (e & (len - 1)) + i1 + i2 + i3;
+      dk[dst] = k[u];
+      dp[dst] = (uint16_t)p[u];
     }
-    i1 += (o1[i1] < k) ? 1 : 0;
-    i2 += (o2[i2] < k) ? 1 : 0;
-    i3 += (o3[i3] < k) ? 1 : 0;
-    dk[qb + (t & (len - 1)) + i1 + i2 + i3] = k;
     __syncthreads();
-    uint64_t *tk = sk; sk = dk; dk = tk;
-    k = sk[t];  // this thread now owns merged position t
+    uint32_t *tk = sk; sk = dk; dk = tk;
+    uint16_t *tp = sp; sp = dp; dp = tp;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {  // merged position e
+      if (u * kFitThreads >= n) continue;
+      k[u] = sk[u * kFitThreads + t];
+      p[u] = sp[u * kFitThreads + t];
+    }
   }
   // runs of equal truncated keys (sorted by position so far) are ranked by
   // their full keys; a run longer than kRunMax sends the block to the full sort
   constexpr int kRunMax = 16;
-  const uint32_t p = (uint32_t)k;
   bool bad = false;
-  if (t < n) {
-    int s0 = t, s1 = t + 1;
-    if (lossy) {
-      const uint32_t hk = (uint32_t)(k >> 32);
-      while (s0 > 0 && t - s0 < kRunMax && (uint32_t)(sk[s0 - 1] >> 32) == hk) --s0;
-      while (s1 < n && s1 - t <= kRunMax && (uint32_t)(sk[s1] >> 32) == hk) ++s1;
-    }
-    if (s1 - s0 > kRunMax) {
-      bad = true;
-    } else if (s1 - s0 == 1) {
-      out[t] = (uint16_t)p;
-    } else {
-      const uint64_t kf = keys[p];
-      int r = 0;
-      for (int u = s0; u < s1; ++u) {
-        const uint32_t pu = (uint32_t)sk[u];
-        r += kp_less(keys[pu], pu, kf, p) ? 1 : 0;
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int e = u * kFitThreads + t;
+    if (e < n) {
+      int s0 = e, s1 = e + 1;
+      if (lossy) {
+        while (s0 > 0 && e - s0 < kRunMax && sk[s0 - 1] == k[u]) --s0;
+        while (s1 < n && s1 - e <= kRunMax && sk[s1] == k[u]) ++s1;
       }
-      out[s0 + r] = (uint16_t)p;
+      if (s1 - s0 > kRunMax) {
+        // a long run is in order when all its full keys are equal (ties of a
+        // quantized hp: ordered by position already), i.e. when no adjacent
+        // pair of it differs; else the block takes the full sort
+        const bool mixed = e > s0 && keys[p[u]] != keys[sp[e - 1]];
+        if (mixed) bad = true;
+        else out[e] = (uint16_t)p[u];
+      } else if (s1 - s0 == 1) {
+        out[e] = (uint16_t)p[u];
+      } else {
+        const uint64_t kf = keys[p[u]];
+        int r = 0;
+        for (int v = s0; v < s1; ++v) {
+          const uint32_t pv = sp[v];
+          r += kp_less(keys[pv], pv, kf, p[u]) ? 1 : 0;
+        }
+        out[s0 + r] = (uint16_t)p[u];
+      }
     }
   }
   return !__syncthreads_or(bad);
@@ -378,13 +430,16 @@ __device__ __forceinline__ PosT *block_sort_perm(const uint64_t *keys, PosT *a, 
                                  uint32_t *cnt, uint32_t *run, FitShared &sm) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (n > 64 && n <= kMergeMax && sizeof(PosT) == 2) {
-    // cnt + run regions (32 KB) hold the two key buffers, b the positions
+    // cnt + run regions (32 KB) hold the merge buffers (12 KB; the full-key
+    // fallback: its two key buffers, b the positions)
     uint64_t *bk = reinterpret_cast<uint64_t *>(cnt);
     // the 32-bit window: from the lowest varying bit, or up to the highest
     const int hb = 63 - __builtin_clzll(vary | 1ull), lb = vary ? __builtin_ctzll(vary) : 0;
     const int shift = max(lb, hb - 31);
-    if (merge_sort_1024_packed(keys, n, shift, shift > lb, reinterpret_cast<uint16_t *>(a), bk,
-                               bk + kFitThreads))
+    uint32_t *kb = reinterpret_cast<uint32_t *>(cnt);
+    uint16_t *pb = reinterpret_cast<uint16_t *>(kb + 2 * kFitThreads);
+    if (merge_sort_packed<1>(keys, n, shift, shift > lb, reinterpret_cast<uint16_t *>(a), kb,
+                             kb + kFitThreads, pb, pb + kFitThreads))
       return a;
     uint16_t *bp = reinterpret_cast<uint16_t *>(b);
     merge_sort_1024(keys, n, reinterpret_cast<uint16_t *>(a), bk, bp, bk + kFitThreads,
@@ -402,11 +457,28 @@ __device__ __forceinline__ PosT *block_sort_perm(const uint64_t *keys, PosT *a, 
     return a;
   }
   if (SMALL) return a;  // n <= kMergeMax: unreachable
+  int passes = 0;
+  for (int shift = 0; shift < 64; shift += 8) passes += ((vary >> shift) & 255u) ? 1 : 0;
+  if (sizeof(PosT) == 2 && n <= 4 * kMergeMax && passes > 2) {
+    // keys in LDS (n <= 4096: bytes [0, 32 KB) of the key region), the merge
+    // buffers (2 x 16 KB keys, 2 x 8 KB positions) above them (the last
+    // overlaps a, which the radix fallback re-initialises), the result in b
+    static_assert(8 * 4 * kMergeMax + 12 * 4 * kMergeMax <= kOffPosB, "merge buffers below b");
+    uint32_t *kb = reinterpret_cast<uint32_t *>(const_cast<uint64_t *>(keys) + 4 * kMergeMax);
+    uint16_t *pb = reinterpret_cast<uint16_t *>(kb + 8 * kMergeMax);
+    const int hb = 63 - __builtin_clzll(vary | 1ull), lb = vary ? __builtin_ctzll(vary) : 0;
+    const int shift = max(lb, hb - 31);
+    if (merge_sort_packed<4>(keys, n, shift, shift > lb, reinterpret_cast<uint16_t *>(b), kb,
+                             kb + 4 * kMergeMax, pb, pb + 4 * kMergeMax))
+      return b;
+  }
   for (int i = threadIdx.x; i < n; i += blockDim.x) a[i] = (PosT)i;
   __syncthreads();
+  STAMP(38);
   for (int shift = 0; shift < 64; shift += 8) {
     if (((vary >> shift) & 255u) == 0) continue;
     radix_pass<PosT>(keys, a, b, n, shift, cnt, run);
+    STAMP(39);
     PosT *t = a; a = b; b = t;
   }
   return a;
@@ -909,11 +981,13 @@ __device__ __forceinline__ void fit_categorical(const FitArgs &A, const FitCtx &
     if (r == m - 1 || keys[perm[r + 1]] != b) seg[2 * b + 1] = r + 1;
   }
   __syncthreads();  // keys are dead from here on
+  STAMP(40);
   // LF weights in sorted order, in parallel (LDS over the keys, or HBM scratch)
   double *ws = m <= kSortCap ? reinterpret_cast<double *>(C.lds + kOffKeys) : A.ob + slot * A.kcap;
   const LfRamp lr = lf_ramp(m, A.lf);
   for (int r = threadIdx.x; r < m; r += blockDim.x) ws[r] = lf_weight(lr, (int64_t)perm[r]);
   __syncthreads();
+  STAMP(41);
   for (int c = threadIdx.x; c < upper; c += blockDim.x) {
     // serial per bin (np.bincount order); loads run 8 ahead of the adds
     double cnt = 0.0;

@@ -208,6 +208,27 @@ def test_parzen_sort_tiers_bit_exact(eng, n, ties):
     np.testing.assert_array_equal(w, ref[0])
 
 
+@pytest.mark.parametrize('n', [900, 1500, 3000, 4096])
+@pytest.mark.parametrize('cluster', [8, 40])
+def test_parzen_merge_sort_truncated_key_runs(eng, n, cluster):
+    """The merge sorts (<= 1024 and <= 4096 observations) order 32 bits of
+    each key: values that differ only below those bits form runs re-ranked by
+    their full keys (<= 16), a longer run of distinct full keys falls back to
+    the radix sort, a long run of equal keys (quantized ties) stays as is."""
+    rng = np.random.RandomState(n + cluster)
+    obs = rng.uniform(-5, 5, n)
+    base = rng.uniform(-5, 5, 3)
+    for j, b in enumerate(base):                      # near-equal clusters, shuffled
+        idx = rng.choice(n, cluster, replace=False)
+        obs[idx] = b + rng.permutation(cluster) * 1e-13 * (j + 1)
+    obs[rng.choice(n, 50, replace=False)] = 2.5       # a long run of equal keys
+    w, mu, sg = eng.parzen_fit(obs, 1.0, 0.25, 10.0)
+    ref = O.parzen_fit(obs, 1.0, 0.25, 10.0, kind='stable')
+    np.testing.assert_array_equal(mu, ref[1])
+    np.testing.assert_array_equal(sg, ref[2])
+    np.testing.assert_array_equal(w, ref[0])
+
+
 @pytest.mark.parametrize('n,gamma,cap', [(1000, 0.25, 25), (20000, 0.25, 25), (5000, 2.0, 1000),
                                          (30000, 1.0, 1000), (50, 10.0, 1000)])
 def test_split_rounds_and_sort_paths(eng, n, gamma, cap):

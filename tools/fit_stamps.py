@@ -37,7 +37,10 @@ def main(cfg, slots):
     P = len(dom.space.labels)
     t0 = st[:2 * P, 0].min()
     print(cfg, 'P=%d N=%d' % (P, losses.size))
-    for slot in range(min(2 * P, slots)):
+    order = range(min(2 * P, slots))
+    if 'TPE_STAMPS_SLOTS' in os.environ:  # the slowest slots, slowest last
+        order = sorted(np.argsort(st[:2 * P, 10] - t0)[-slots:], key=lambda s: st[s, 10])
+    for slot in order:
         row = st[slot]
         h = dom.space.hps[slot // 2]
         marks = ['%s=%.1f' % (PH[i], (row[i] - row[0]) / 100.0) for i in [11, 12, 13, 14, 15] + sorted(k for k in PH if k < 11)
@@ -48,7 +51,8 @@ def main(cfg, slots):
     sub = {16: 'sd.zero', 17: 'sd.hist', 18: 'sd.bar1', 19: 'sd.scan', 20: 'sd.bar2',
            21: 'ms.load', 22: 'ms.bitonic64', 23: 'ms.bar', 24: 'ms.L64', 25: 'ms.L128',
            26: 'ms.L256', 27: 'ms.L512', 28: 'np.plan', 29: 'np.leaves', 30: 'np.end',
-           31: 'k.zero', 32: 'k.load', 33: 'k.wred', 34: 'k.bar', 35: 'g.load', 36: 'g.scan', 37: 'g.write'}
+           31: 'k.zero', 32: 'k.load', 33: 'k.wred', 34: 'k.bar', 35: 'g.load', 36: 'g.scan', 37: 'g.write',
+           38: 'rs.init', 39: 'rs.pass', 40: 'cat.seg', 41: 'cat.lfw'}
     for slot in range(min(2 * P, 4)):
         row = st[slot]
         print('slot %d last sub-phase stamps (us from slot start): ' % slot + ' '.join(
@@ -59,5 +63,6 @@ def main(cfg, slots):
 
 
 if __name__ == '__main__':
+    # usage: fit_stamps.py [config ...]; TPE_STAMPS_SLOTS=n prints the n slowest slots
     for c in sys.argv[1:] or ['cfg2']:
-        main(c, 40)
+        main(c, int(os.environ.get('TPE_STAMPS_SLOTS', '40')))
