@@ -16,14 +16,11 @@
 
 #include "tpe_internal.hpp"
 
-#ifndef TPE_LAT_SIDE
-#define TPE_LAT_SIDE 0  // 1: k_lattice on a side stream beside k_draw (fork / join)
-#endif
-
 using namespace tpe;
 
 static int lse_shift_min();
 static bool compact_on();
+static bool lat_side_on();
 static bool sort_by_rows();
 static bool wave_tiles_on();
 static bool small_sort_on();
@@ -652,7 +649,7 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
   // a small one-chunk draw whose tables fit kFuseTab runs in extra blocks of
   // the lattice launch (both only need the fitted mixtures): one launch less
   // and the draw hidden behind the lattice points
-  const bool fuse_draw = !TPE_LAT_SIDE && lat_level && n_lat <= kLatJobs && table_draw &&
+  const bool fuse_draw = lat_level && n_lat <= kLatJobs && table_draw &&
                          kmax <= kFuseTab && chunk >= n_cand &&
                          n_cand * n_sug * n_level < ((int64_t)1 << 22);
   if (lat_level) {
@@ -661,22 +658,23 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
     for (int i = n_lat; i < n_level; ++i)
       erf_level |= kinds[i] == KIND_ERF_G || kinds[i] == KIND_ERF_L;
   }
+  // the lattice needs only the fitted mixtures: unless it carries the draw
+  // (fuse_draw), it runs on a side stream beside the candidate draw (fork /
+  // join events; a parallel branch of the captured graph), and the scoring
+  // launch waits for it
+  const bool lat_side = lat_level && !fuse_draw && lat_side_on();
   if (lat_level && !fuse_draw) {
-    // the lattice needs only the fitted mixtures: it runs on a side stream
-    // beside the candidate draw (fork / join events; a parallel branch of the
-    // captured graph), and the scoring launch waits for it
     ScoreArgs la = base_args(p, n_sug);
     la.level_hps = lvl;
     la.n_slots = n_level;
     la.slot_rows = slot_rows;
     la.compact = compact ? 1 : 0;
-#if TPE_LAT_SIDE
-    hipStream_t sl = h->aux[0];
-    CKH(hipEventRecord(p->ev_fork, st));
-    CKH(hipStreamWaitEvent(sl, p->ev_fork, 0));
-#else
     hipStream_t sl = st;
-#endif
+    if (lat_side) {
+      sl = h->aux[0];
+      CKH(hipEventRecord(p->ev_fork, st));
+      CKH(hipStreamWaitEvent(sl, p->ev_fork, 0));
+    }
     tpe_plan::Prof *pr = nullptr;
     if (p->prof_cap > 0 && p->prof[1].n < p->prof_cap) pr = &p->prof[1];
     if (pr) CKH(hipEventRecord(pr->a[pr->n], sl));
@@ -687,11 +685,9 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
       pr->pairs[pr->n] = (double)level;
       pr->n++;
     }
-#if TPE_LAT_SIDE
-    CKH(hipEventRecord(p->ev_join[0], sl));
-#endif
+    if (lat_side) CKH(hipEventRecord(p->ev_join[0], sl));
   }
-  bool joined = !(TPE_LAT_SIDE && lat_level);
+  bool joined = !lat_side;
   // log-sum-exp tiles: two candidate rows per lane, unless that leaves fewer
   // than ~3 blocks per CU (then whole-block work units are few and coarse, and
   // a CU with one more of them than its neighbours sets the launch time):
@@ -1658,6 +1654,14 @@ static bool wave_tiles_on() {
 // launch costs more than that (suggest 70 -> 78 us)
 // compact (active-slot) grids of conditional levels; TPE_COMPACT=0 turns
 // them off (A/B measurements)
+static bool lat_side_on() {  // TPE_LAT_SIDE=0: the lattice on the main stream
+  static const bool on = [] {
+    const char *e = std::getenv("TPE_LAT_SIDE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 static bool compact_on() {
   static const bool on = [] {
     const char *e = std::getenv("TPE_COMPACT");
