@@ -35,7 +35,9 @@ def main(cfg, n_cand):
     plan.set_history(losses, vals, active)
     for i in range(5):
         plan.fit(gamma=0.25, prior_weight=1.0, lf=25)
-        plan.suggest([7 + i], n_cand, fetch=False)
+        # TPE_STAMPS_LEVEL=l: stop after level l (its launch is the last one)
+        plan.suggest([7 + i], n_cand, level=int(os.environ.get('TPE_STAMPS_LEVEL', '-1')),
+                     fetch=False)
     eng.lib.tpe_synchronize(eng.h)
     buf = (C.c_ulonglong * (8192 * 4))()
     assert eng.lib.tpe_debug_score_stamps(buf) == 0
