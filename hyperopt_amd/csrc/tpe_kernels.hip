@@ -12,6 +12,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "tpe_draw.hpp"
 
@@ -29,6 +30,7 @@ constexpr int kSortMax = 8192;  // candidates per bucketing chunk
 // the per-draw rejection sampler runs (!TAB), in a kernel of its own so the
 // table path keeps its small register footprint.
 constexpr int kDrawThreads = 256;
+constexpr int kWideDrawThreads = 1024;
 template <bool TAB>
 __global__ __launch_bounds__(kDrawThreads) void k_draw(ScoreArgs A) {
   if constexpr (TAB) {
@@ -60,10 +62,10 @@ __device__ __forceinline__ int slot_kind(const ScoreArgs &A, int slot) {
   return -1;
 }
 
-template <int CAP, bool EXT>
+template <int CAP, int NT, bool EXT>
 __device__ __forceinline__ void sorted_block(const ScoreArgs &A, int32_t *__restrict__ pos_out,
                                              const double *__restrict__ src,
-                                             SortedDrawLds<CAP, kDrawThreads> &L) {
+                                             SortedDrawLds<CAP, NT> &L) {
   const int s = blockIdx.z;
   const int slot = row_slot(A, s, 0, A.n_slots, blockIdx.y);
   if (slot < 0) return;
@@ -72,7 +74,7 @@ __device__ __forceinline__ void sorted_block(const ScoreArgs &A, int32_t *__rest
       !hp_active(A.hps[hp], A.results + (int64_t)s * A.n_hp, A.cond_parent, A.cond_branch))
     return;
   const int kind = slot_kind(A, slot);
-  sorted_block_body<CAP, kDrawThreads, EXT>(
+  sorted_block_body<CAP, NT, EXT>(
       A, slot, s, (int64_t)blockIdx.x * kSortedBlock,
       kind_lse(kind) || kind == KIND_ERF_G || kind == KIND_ERF_L, kind_logn(kind), pos_out, src,
       L);
@@ -81,13 +83,23 @@ __device__ __forceinline__ void sorted_block(const ScoreArgs &A, int32_t *__rest
 template <int CAP>
 __global__ __launch_bounds__(kDrawThreads) void k_draw_sorted(ScoreArgs A, int32_t *__restrict__ pos_out) {
   __shared__ SortedDrawLds<CAP, kDrawThreads> L;
-  sorted_block<CAP, false>(A, pos_out, nullptr, L);
+  sorted_block<CAP, kDrawThreads, false>(A, pos_out, nullptr, L);
+}
+
+// The same blocks on 1024 threads, for launches of too few blocks to fill the
+// CUs (the block's 4096 draws are split 4 x finer; the scatter is stable, so
+// the output does not depend on the block size)
+template <int CAP>
+__global__ __launch_bounds__(kWideDrawThreads) void k_draw_sorted_wide(ScoreArgs A,
+                                                                       int32_t *__restrict__ pos_out) {
+  __shared__ SortedDrawLds<CAP, kWideDrawThreads> L;
+  sorted_block<CAP, kWideDrawThreads, false>(A, pos_out, nullptr, L);
 }
 
 __global__ __launch_bounds__(kDrawThreads) void k_sort_ext(ScoreArgs A, const double *__restrict__ src,
                                                            int32_t *__restrict__ pos_out) {
   __shared__ SortedDrawLds<1, kDrawThreads> L;
-  sorted_block<1, true>(A, pos_out, src, L);
+  sorted_block<1, kDrawThreads, true>(A, pos_out, src, L);
 }
 
 // Bucket each 8192-candidate chunk of the erf-kind hps by value (counting
@@ -553,13 +565,30 @@ hipError_t launch_draw(const ScoreArgs &a, bool table, hipStream_t st) {
   return hipGetLastError();
 }
 
+static bool wide_draw_on() {  // TPE_WIDE_DRAW=0: always 256-thread sorted-draw blocks
+  static const bool on = [] {
+    const char *e = std::getenv("TPE_WIDE_DRAW");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 hipError_t launch_draw_sorted(const ScoreArgs &a, bool small_table, int32_t *pos_out,
                               hipStream_t st) {
   if (a.n_slots <= 0 || a.n_suggest <= 0 || a.n_cand <= 0) return hipSuccess;
   const unsigned gx = (unsigned)((a.n_cand + kSortedBlock - 1) / kSortedBlock);
   const dim3 g(gx, (unsigned)a.slot_rows, a.n_suggest);
-  if (small_table) k_draw_sorted<kFuseTab><<<g, kDrawThreads, 0, st>>>(a, pos_out);
-  else k_draw_sorted<kTabCap><<<g, kDrawThreads, 0, st>>>(a, pos_out);
+  // fewer blocks than ~2 per CU: 1024-thread blocks (a 256-thread block is 1
+  // wave per SIMD; the launch is then bound by one block's latency)
+  const bool wide = (int64_t)gx * a.slot_rows * a.n_suggest <= 2 * kNumCUs && wide_draw_on();
+  if (wide) {
+    if (small_table) k_draw_sorted_wide<kFuseTab><<<g, kWideDrawThreads, 0, st>>>(a, pos_out);
+    else k_draw_sorted_wide<kTabCap><<<g, kWideDrawThreads, 0, st>>>(a, pos_out);
+  } else if (small_table) {
+    k_draw_sorted<kFuseTab><<<g, kDrawThreads, 0, st>>>(a, pos_out);
+  } else {
+    k_draw_sorted<kTabCap><<<g, kDrawThreads, 0, st>>>(a, pos_out);
+  }
   return hipGetLastError();
 }
 
