@@ -376,3 +376,25 @@ def test_config2_sorted_draw_winner_values_regenerate():
         res = plan.suggest([seed], n)[0]
         assert res['active'].all()
         _check_winners(dom, plan, res, seed, n, obs, 'cfg2 seed %d' % seed)
+
+
+def test_config3_wide_and_narrow_sorted_draws_agree():
+    """Config 3 (conditional, 1e5 candidates): a single suggestion's level-2
+    sorted draw is a launch of <= 2 blocks per CU (k_draw_sorted_wide,
+    1024-thread blocks); a batch of 4 is not (256-thread blocks).  The
+    draw and its bucket scatter do not depend on the block size, so the
+    batch's first suggestion equals the single one bit for bit, and every
+    winner's value regenerates from its index."""
+    import bench
+    dom, losses, vals, act = bench.build_workload('cfg3')
+    hps, conds, pprior = dom.space.engine_tables()
+    plan = E.Plan(E.default_engine(), hps, conds, pprior, max_trials=losses.size)
+    plan.set_history(losses, vals, act)
+    plan.fit()
+    n = 100000
+    one = plan.suggest([11], n)[0]
+    four = plan.suggest([11, 12, 13, 14], n)[0]
+    for f in ('active', 'index', 'value', 'score'):
+        np.testing.assert_array_equal(one[f], four[f], err_msg=f)
+    obs = _oracle_obs(dom, losses, vals, act)
+    _check_winners(dom, plan, one, 11, n, obs, 'cfg3 seed 11')
