@@ -53,7 +53,8 @@ def main(cfg, slots):
            26: 'ms.L256', 27: 'ms.L512', 28: 'np.plan', 29: 'np.leaves', 30: 'np.end',
            31: 'k.zero', 32: 'k.load', 33: 'k.wred', 34: 'k.bar', 35: 'g.load', 36: 'g.scan', 37: 'g.write',
            38: 'rs.init', 39: 'rs.pass', 40: 'cat.seg', 41: 'cat.lfw'}
-    for slot in range(min(2 * P, 4)):
+    slowest = int(np.argmax(st[:2 * P, 10] - st[:2 * P, 0]))
+    for slot in sorted(set(range(min(2 * P, 4))) | {slowest}):
         row = st[slot]
         print('slot %d last sub-phase stamps (us from slot start): ' % slot + ' '.join(
             '%s=%.2f' % (nm, (row[i] - row[0]) / 100.0) for i, nm in sub.items() if row[i] >= row[0]))
