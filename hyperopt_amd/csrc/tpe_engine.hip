@@ -21,6 +21,7 @@ using namespace tpe;
 static int lse_shift_min();
 static bool compact_on();
 static bool lat_side_on();
+static bool cat_counting_on();
 static bool sort_by_rows();
 static bool wave_tiles_on();
 static bool small_sort_on();
@@ -564,6 +565,7 @@ FitArgs fit_args(tpe_plan *p, int32_t n_below, double prior_weight, int32_t lf) 
   a.ld = p->ncap;
   a.n_below = n_below;
   a.lf = lf;
+  a.cat_counting = cat_counting_on() ? 1 : 0;
   a.prior_weight = prior_weight;
   a.pprior = p->d_pprior;
   a.mw = p->d_mw;
@@ -1654,6 +1656,14 @@ static bool wave_tiles_on() {
 // launch costs more than that (suggest 70 -> 78 us)
 // compact (active-slot) grids of conditional levels; TPE_COMPACT=0 turns
 // them off (A/B measurements)
+static bool cat_counting_on() {  // TPE_CAT_COUNT=0: categorical fits always sort
+  static const bool on = [] {
+    const char *e = std::getenv("TPE_CAT_COUNT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 static bool lat_side_on() {  // TPE_LAT_SIDE=0: the lattice on the main stream
   static const bool on = [] {
     const char *e = std::getenv("TPE_LAT_SIDE");

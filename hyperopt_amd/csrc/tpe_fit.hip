@@ -963,12 +963,17 @@ __device__ __forceinline__ void fit_continuous(const FitArgs &A, const FitCtx &C
 // perm: observations stably sorted by category -> one segment per bin whose
 // serial sum keeps the reference's rounding.
 // ------------------------------------------------------------------------
+// the per-bin sums, pseudocounts and normalisation once ws holds the LF
+// weights grouped by bin (bin c: ws[seg[2c], seg[2c+1]) in observation order)
+__device__ __forceinline__ void categorical_tail(const FitArgs &A, FitShared &sm, const tpe_hp &H,
+                                                 int64_t slot, const int *seg, const double *ws);
+
 template <typename PosT>
 __device__ __forceinline__ void fit_categorical(const FitArgs &A, const FitCtx &C, FitShared &sm,
                                 const tpe_hp &H, int64_t slot, const uint64_t *keys,
                                 const PosT *perm, int m) {
   const int upper = H.upper;
-  double *w = A.mw + slot * A.kcap, *mu = A.mmu + slot * A.kcap, *sg = A.msig + slot * A.kcap;
+  double *mu = A.mmu + slot * A.kcap;
   // segment bounds per bin: LDS (cnt/run region) when they fit, else the
   // (not yet written) global mu array of the slot
   int *seg = upper <= 4096 ? reinterpret_cast<int *>(C.lds + kOffCnt) : reinterpret_cast<int *>(mu);
@@ -988,6 +993,85 @@ __device__ __forceinline__ void fit_categorical(const FitArgs &A, const FitCtx &
   for (int r = threadIdx.x; r < m; r += blockDim.x) ws[r] = lf_weight(lr, (int64_t)perm[r]);
   __syncthreads();
   STAMP(41);
+  categorical_tail(A, sm, H, slot, seg, ws);
+}
+
+// Categorical fit of a large history (m <= kSortCap observations, keys in
+// LDS) over few bins (upper <= 64): no sort.  A stable counting pass puts each
+// observation's LF weight straight at its place in the bin-grouped order:
+// every wave takes a contiguous run of the observations, counts its bins by
+// one ballot per bin and 64 observations, and scatters with the bin's base
+// (bins in order, waves in order within a bin) plus the rank among the equal
+// keys of its 64 -- the order the stable sort gives, so the sums are the same.
+constexpr int kCatFastBins = 64;
+constexpr int kCatFastChunks = (kSortCap + kFitThreads - 1) / kFitThreads;  // 64-runs per wave
+__device__ __forceinline__ void fit_categorical_counting(const FitArgs &A, const FitCtx &C,
+                                                         FitShared &sm, const tpe_hp &H,
+                                                         int64_t slot, int m) {
+  const int upper = H.upper;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t *keys = reinterpret_cast<const uint64_t *>(C.lds + kOffKeys);
+  int *seg = reinterpret_cast<int *>(C.lds + kOffCnt);                 // [2 * upper]
+  uint32_t *wc = reinterpret_cast<uint32_t *>(C.lds + kOffRun);        // [16 waves][64 bins]
+  const int per = (m + kFitWaves * 64 - 1) / (kFitWaves * 64) * 64;    // <= 64 * kCatFastChunks
+  const int r0 = wv * per;
+  // this wave's keys into registers (bin, or -1), then its per-bin counts
+  int kr[kCatFastChunks];
+  uint32_t cnt = 0;
+#pragma unroll
+  for (int q = 0; q < kCatFastChunks; ++q) {
+    const int i = r0 + q * 64 + lane;
+    const bool v = q * 64 < per && i < m;
+    const uint64_t k = v ? keys[i] : ~0ull;
+    kr[q] = k < (uint64_t)upper ? (int)k : -1;
+    if (q * 64 < per) {
+      for (int b = 0; b < upper; ++b) {
+        const uint64_t bal = __ballot(kr[q] == b);
+        if (lane == b) cnt += (uint32_t)__popcll(bal);
+      }
+    }
+  }
+  wc[wv * kCatFastBins + lane] = lane < upper ? cnt : 0u;
+  __syncthreads();  // every key is in registers: the key region is free for ws
+  // lane b: bin b's start (bins before it, all waves) + its count in waves before this one
+  uint32_t tot = 0, mine = 0;
+#pragma unroll
+  for (int w = 0; w < kFitWaves; ++w) {
+    const uint32_t c = wc[w * kCatFastBins + lane];
+    tot += c;
+    mine += w < wv ? c : 0u;
+  }
+  const uint32_t start = wave_excl_scan_u32(tot);
+  if (wv == 0 && lane < upper) {
+    seg[2 * lane] = (int)start;
+    seg[2 * lane + 1] = (int)(start + tot);
+  }
+  uint32_t run = start + mine;
+  double *ws = reinterpret_cast<double *>(C.lds + kOffKeys);
+  const LfRamp lr = lf_ramp(m, A.lf);
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+#pragma unroll
+  for (int q = 0; q < kCatFastChunks; ++q) {
+    if (q * 64 >= per) break;
+    uint32_t rank = 0, inc = 0;
+    for (int b = 0; b < upper; ++b) {
+      const uint64_t bal = __ballot(kr[q] == b);
+      if (kr[q] == b) rank = (uint32_t)__popcll(bal & lt);
+      if (lane == b) inc = (uint32_t)__popcll(bal);
+    }
+    const uint32_t base = (uint32_t)__shfl((int)run, kr[q] < 0 ? 0 : kr[q], 64);
+    if (kr[q] >= 0) ws[base + rank] = lf_weight(lr, (int64_t)(r0 + q * 64 + lane));
+    run += inc;
+  }
+  __syncthreads();
+  STAMP(41);
+  categorical_tail(A, sm, H, slot, seg, ws);
+}
+
+__device__ __forceinline__ void categorical_tail(const FitArgs &A, FitShared &sm, const tpe_hp &H,
+                                                 int64_t slot, const int *seg, const double *ws) {
+  const int upper = H.upper;
+  double *w = A.mw + slot * A.kcap, *mu = A.mmu + slot * A.kcap, *sg = A.msig + slot * A.kcap;
   for (int c = threadIdx.x; c < upper; c += blockDim.x) {
     // serial per bin (np.bincount order); loads run 8 ahead of the adds
     double cnt = 0.0;
@@ -1176,7 +1260,18 @@ __device__ __forceinline__ void fit_slot(const FitArgs &A, unsigned char *dyn_ld
 
   uint32_t *cnt = reinterpret_cast<uint32_t *>(dyn_lds + kOffCnt);
   uint32_t *run = reinterpret_cast<uint32_t *>(dyn_lds + kOffRun);
-  if (lds_sort) {
+  bool done = false;
+  if constexpr (!SMALL) {
+    // categorical over few bins, more observations than the merge sort's:
+    // no sort (fit_categorical_counting)
+    if (lds_sort && cat && H.upper <= kCatFastBins && m > kMergeMax && A.cat_counting) {
+      STAMP(3);
+      fit_categorical_counting(A, C, sm, H, slot, m);
+      done = true;
+    }
+  }
+  if (done) {
+  } else if (lds_sort) {
     const uint16_t *perm = block_sort_perm<uint16_t, SMALL>(
         lk, reinterpret_cast<uint16_t *>(dyn_lds + kOffPosA),
         reinterpret_cast<uint16_t *>(dyn_lds + kOffPosB), m, vary, cnt, run, sm);

@@ -226,6 +226,8 @@ struct FitArgs {
   int64_t ld;                // row stride of vals / active (the plan's trial capacity)
   int32_t n_below;
   int32_t lf;
+  int32_t cat_counting;      // categorical fits of > 1024 observations without the sort
+  int32_t pad0;
   double prior_weight;
   const double *pprior;
   double *mw, *mmu, *msig;   // [2P][kcap] fitted mixtures

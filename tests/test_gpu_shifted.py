@@ -398,3 +398,31 @@ def test_config3_wide_and_narrow_sorted_draws_agree():
         np.testing.assert_array_equal(one[f], four[f], err_msg=f)
     obs = _oracle_obs(dom, losses, vals, act)
     _check_winners(dom, plan, one, 11, n, obs, 'cfg3 seed 11')
+
+
+def test_config3_categorical_posteriors_bit_exact():
+    """Config 3's categorical hps at N = 1e4 (the root choice: ~1e4 above-side
+    observations over 7 bins; each branch's choices ~1.4e3): the plan's fit
+    (counting path, no sort, for > 1024 observations over <= 64 bins) gives
+    the oracle's posterior bit for bit on both sides (np.bincount order of
+    the LF-weighted counts, tpe.py:573-589)."""
+    import bench
+    from oracle import tpe_oracle as O
+    dom, losses, vals, act = bench.build_workload('cfg3')
+    hps, conds, pprior = dom.space.engine_tables()
+    plan = E.Plan(E.default_engine(), hps, conds, pprior, max_trials=losses.size)
+    plan.set_history(losses, vals, act)
+    plan.fit()
+    obs = _oracle_obs(dom, losses, vals, act)
+    n_checked = 0
+    for h in dom.space.hps:
+        t = hps[h.index]
+        if t.family != E.CAT or t.flags & E.PCHOICE:
+            continue
+        for side in (0, 1):
+            o = obs[h.label][side]
+            w = plan.mixture(h.index, side)[0]
+            ref = O.categorical_posterior(o, t.upper, 1.0)
+            np.testing.assert_array_equal(w[:t.upper], ref, err_msg='%s side %d' % (h.label, side))
+            n_checked += o.size > 1024
+    assert n_checked >= 2
