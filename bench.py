@@ -373,6 +373,7 @@ def main():
     torch.cuda.synchronize()
     plan.set_history_device(d_losses.data_ptr(), d_vals.data_ptr(), d_act.data_ptr(),
                             losses.size)
+    plan.engine.synchronize()  # the copies are stream-ordered: done before any fit
 
     mode = C['mode'] if (world > 1 or args.parallelism == 'sharded') else 'single'
     sharded = parallel.ShardedSuggest(plan) if mode == 'sharded' else None

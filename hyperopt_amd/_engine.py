@@ -222,6 +222,11 @@ class Engine(object):
             raise ValueError(msg)
         raise EngineError('TPE engine error %d: %s' % (rc, msg))
 
+    def synchronize(self):
+        """Wait for all of this engine's device work (tpe_synchronize)."""
+        with self.lock:
+            self.check(self.lib.tpe_synchronize(self.h))
+
     def microbench(self, which):
         r = C.c_double(0)
         with self.lock:

@@ -606,6 +606,14 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
               int64_t cand_begin, hipStream_t st) {
   const int32_t n_level = (int32_t)p->levels[level].size();
   const int32_t *lvl = p->d_level_hps + p->level_off[level];
+  if (n_cand == 0) {
+    // no candidates (an empty shard of a small suggest, n_EI_candidates = 0):
+    // broadcast_best of no samples is [] (tpe.py:750-759) -- every hp of the
+    // level gets the neutral record (NaN, NaN, -1, inactive), which k_merge
+    // treats as "nothing here" (a merge of zero records writes exactly that)
+    if (n_level > 0) CKH(launch_merge(lvl, n_level, (int32_t)n_sug, p->P, 0, nullptr, p->d_results, st));
+    return TPE_OK;
+  }
   bool erf_level = false;
   std::vector<int> kinds;
   // largest below mixture the draw can meet: the LDS table sampler fits it?
@@ -708,6 +716,9 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
       for (int &k : kinds)
         k = k == KIND_LSE_G ? KIND_LSE_G1 : k == KIND_LSE_L ? KIND_LSE_L1 : k;
   }
+  // every exit of the chunk loop (errors included) joins the lattice side
+  // stream back, so a failed call never leaves a captured graph forked
+  auto chunks = [&]() -> int {
   int64_t c0 = 0;
   do {
     const int64_t cn = std::min(chunk, n_cand - c0);
@@ -790,6 +801,13 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
     c0 += cn;
   } while (c0 < n_cand);
   return TPE_OK;
+  };
+  const int rc = chunks();
+  if (!joined) {
+    const hipError_t e = hipStreamWaitEvent(st, p->ev_join[0], 0);
+    if (!rc && e != hipSuccess) return fail(h, TPE_E_HIP, "join of the lattice side stream");
+  }
+  return rc;
 }
 
 // Externally supplied candidates of one hp (parity / operator path).

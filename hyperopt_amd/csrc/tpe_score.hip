@@ -779,7 +779,18 @@ struct ScoreSmem {
   double2 merged[2][kRMax][64];         // merged per (mixture, candidate row)
   double best_s[kWaves], best_v[kWaves];  // wave tiles: each wave's argmax
   int64_t best_i[kWaves];
+#ifdef TPE_REREAD
+  int64_t best_li[kWaves];
+#endif
 };
+
+#ifdef TPE_REREAD
+// diagnostic build only (make dbg3; tools/reread_diag.py): per hp of
+// suggestion 0, the winner's value and index and what a finalize-time re-read
+// of its candidate finds at the addresses it could have taken
+__device__ double g_reread[512][20];
+__device__ int64_t g_tile_li[1 << 20][2];
+#endif
 
 template <int KIND, bool CENSUS>
 __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, int slot, int tile,
@@ -999,6 +1010,9 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
   // ---- finalize the tile (wave 0): lpdfs, EI, argmax (numpy semantics)
   double best_s = NAN, best_v = NAN;
   int64_t best_i = -1;
+#ifdef TPE_REREAD
+  int64_t best_li = -1;  // the bucketed slot of the lane's best (diagnostic build)
+#endif
 #pragma unroll
   for (int r = 0; r < KR; ++r) {
     if (!valid[r]) continue;
@@ -1032,8 +1046,49 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
     if (A.out_la) A.out_la[lo] = lpa;
     const double sc = lpb - lpa;
     const int64_t gi = A.cand_begin + lo;
-    if (better(sc, gi, best_s, best_i)) { best_s = sc; best_v = x[r]; best_i = gi; }
+    if (better(sc, gi, best_s, best_i)) {
+      best_s = sc; best_v = x[r]; best_i = gi;
+#ifdef TPE_REREAD
+      best_li = li[r];
+#endif
+    }
   }
+#ifdef TPE_REREAD
+  // the same reductions carrying the winner's bucketed slot, plus the two
+  // slots a re-read that does not carry it would take: lane 0's own best
+  // (not carried through the wave argmax) and wave 0's winner (not carried
+  // through the block argmax of the wave tiles)
+  const int64_t dbg_own0 = __shfl(best_li, 0, 64);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double os = __shfl_xor(best_s, o, 64), ov = __shfl_xor(best_v, o, 64);
+    const int64_t oi = __shfl_xor(best_i, o, 64), ol = __shfl_xor(best_li, o, 64);
+    if (better(os, oi, best_s, best_i)) { best_s = os; best_v = ov; best_i = oi; best_li = ol; }
+  }
+  int64_t dbg_w0 = best_li;
+  if constexpr (WT) {
+    if (lane == 0) {
+      sm.best_s[wave] = best_s; sm.best_v[wave] = best_v; sm.best_i[wave] = best_i;
+      sm.best_li[wave] = best_li;
+    }
+    __syncthreads();
+    if (wave != 0) return;
+    dbg_w0 = best_li;
+    const int w = lane < kWaves ? lane : 0;
+    best_s = sm.best_s[w]; best_v = sm.best_v[w]; best_i = lane < kWaves ? sm.best_i[w] : -1;
+    best_li = sm.best_li[w];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double os = __shfl_xor(best_s, o, 64), ov = __shfl_xor(best_v, o, 64);
+      const int64_t oi = __shfl_xor(best_i, o, 64), ol = __shfl_xor(best_li, o, 64);
+      if (better(os, oi, best_s, best_i)) { best_s = os; best_v = ov; best_i = oi; best_li = ol; }
+    }
+  }
+  if (lane == 0 && s == 0 && (int64_t)hp * A.pstride + tile < (1 << 20)) {
+    g_tile_li[(int64_t)hp * A.pstride + tile][0] = dbg_w0;
+    g_tile_li[(int64_t)hp * A.pstride + tile][1] = dbg_own0;
+  }
+#else
   wave_best(best_s, best_v, best_i);
   if constexpr (WT) {  // the block's argmax over its wave tiles (better() orders ties)
     if (lane == 0) { sm.best_s[wave] = best_s; sm.best_v[wave] = best_v; sm.best_i[wave] = best_i; }
@@ -1043,6 +1098,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
     best_s = sm.best_s[w]; best_v = sm.best_v[w]; best_i = lane < kWaves ? sm.best_i[w] : -1;
     wave_best(best_s, best_v, best_i);
   }
+#endif
   Partial *pbase = A.partial + ((int64_t)s * A.n_hp + hp) * A.pstride;
   int is_last = 0;
   if (lane == 0) {
@@ -1055,6 +1111,9 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
     __hip_atomic_store(rec + 0, dbits(best_s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(rec + 1, dbits(best_v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(rec + 2, (uint64_t)best_i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifdef TPE_REREAD
+    __hip_atomic_store(rec + 3, (uint64_t)best_li, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     gu32 *tk = (gu32 *)(uintptr_t)(A.ticket + (int64_t)s * A.n_hp + hp);
     const uint32_t t = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1067,19 +1126,81 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the loads below the ticket
   double fs = NAN, fv = NAN;
   int64_t fi = -1;
+#ifdef TPE_REREAD
+  int64_t ft = -1;
+#endif
   for (int i = lane; i < ntiles; i += 64) {
     gu64 *rec = (gu64 *)(uintptr_t)(pbase + i);
     const double qs = bitsd(__hip_atomic_load(rec + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     const double qv = bitsd(__hip_atomic_load(rec + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     const int64_t qi = (int64_t)__hip_atomic_load(rec + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifdef TPE_REREAD
+    if (better(qs, qi, fs, fi)) { fs = qs; fv = qv; fi = qi; ft = i; }
+#else
     if (better(qs, qi, fs, fi)) { fs = qs; fv = qv; fi = qi; }
+#endif
   }
+#ifdef TPE_REREAD
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double os = __shfl_xor(fs, o, 64), ov = __shfl_xor(fv, o, 64);
+    const int64_t oi = __shfl_xor(fi, o, 64), ot = __shfl_xor(ft, o, 64);
+    if (better(os, oi, fs, fi)) { fs = os; fv = ov; fi = oi; ft = ot; }
+  }
+  if (lane == 0) {
+    Partial *rr = A.results + (int64_t)s * A.n_hp + hp;
+    if (!(A.accumulate && better(rr->score, rr->index, fs, fi))) {
+      *rr = Partial{fs, fv, fi, 1, 0};
+      if (s == 0 && ft >= 0 && hp < 512) {
+        // the winner's slot as carried through every reduction, and the
+        // values a finalize-time re-read finds at each candidate address
+        gu64 *rec = (gu64 *)(uintptr_t)(pbase + ft);
+        const int64_t lt = (int64_t)__hip_atomic_load(rec + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int64_t tix = (int64_t)hp * A.pstride + ft;
+        const int64_t lw0 = tix < (1 << 20) ? g_tile_li[tix][0] : -1;
+        const int64_t lown = tix < (1 << 20) ? g_tile_li[tix][1] : -1;
+        const volatile double *vc = cand;
+        const int64_t pos = fi - A.cand_begin;
+        double *d = g_reread[hp];
+        d[0] = fv;
+        d[1] = (double)fi;
+        d[2] = (double)lt;
+        d[3] = (lt >= 0 && lt < A.n_cand) ? vc[lt] : NAN;
+        d[4] = (lt >= 0 && lt < A.n_cand && cpos) ? (double)cpos[lt] : NAN;
+        d[5] = (pos >= 0 && pos < A.n_cand) ? vc[pos] : NAN;
+        d[6] = (lw0 >= 0 && lw0 < A.n_cand) ? vc[lw0] : NAN;
+        d[7] = (lown >= 0 && lown < A.n_cand) ? vc[lown] : NAN;
+        d[8] = (double)A.cand_begin;
+        d[9] = (double)ft;
+        d[10] = (double)lw0;
+        d[11] = (double)lown;
+        d[12] = (double)(uintptr_t)cand;
+        d[13] = (double)(uintptr_t)A.partial;
+        d[14] = (double)A.n_cand;
+        d[15] = (double)(uintptr_t)cpos;
+        // the same lane's other candidate row (slot bit 64 of a two-row wave tile)
+        const int64_t lr = lt ^ 64;
+        d[16] = (lt >= 0 && lr < A.n_cand) ? vc[lr] : NAN;
+      }
+    }
+  }
+#else
   wave_best(fs, fv, fi);
   if (lane == 0) {
     Partial *rr = A.results + (int64_t)s * A.n_hp + hp;
     if (!(A.accumulate && better(rr->score, rr->index, fs, fi))) *rr = Partial{fs, fv, fi, 1, 0};
   }
+#endif
 }
+
+#ifdef TPE_REREAD
+}  // namespace tpe
+extern "C" int tpe_debug_reread(double *out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(tpe::g_reread), sizeof(tpe::g_reread)) == hipSuccess
+             ? 0 : -5;
+}
+namespace tpe {
+#endif
 
 #ifdef TPE_STAMPS
 }  // namespace tpe

@@ -76,7 +76,7 @@ class TrialHistory(object):
         self.tids = []
         self.docs = []          # the document of each row
         self._row = {}          # id(doc) -> row (incremental mode)
-        self._dropped = {}      # id(doc) -> doc: visible documents without a row
+        self._dropped = {}      # id(doc) -> (doc, its loss then): visible documents without a row
         self._pending = set()   # rows with loss +inf (new / running / failed)
         self._owner = None      # weakref to the Trials synced
         self._epoch = None
@@ -162,7 +162,7 @@ class TrialHistory(object):
             if k in done:
                 continue
             done.add(k)
-            if k in self._dropped and self._dropped[k] is doc:
+            if k in self._dropped and self._dropped[k][0] is doc:
                 # a visible document the last rebuild left out (a first NaN
                 # loss, or a duplicate tid that lost the dedupe) changed: it
                 # may belong in the history now
@@ -180,7 +180,14 @@ class TrialHistory(object):
                 self._loss_dirty = min(self._loss_dirty, r)
             self._put_row(r, tid, loss, v, a, doc)
         # safety net for results mutated in place (no journal entry): the
-        # losses of the few rows still waiting for one are re-read
+        # losses of the few rows still waiting for one are re-read, and those
+        # of the few documents the last rebuild left out (a NaN loss that is
+        # now a number, a duplicate tid whose loss now wins the dedupe)
+        if len(self._dropped) <= _PENDING_RECHECK:
+            for d, l0 in self._dropped.values():
+                loss = _loss_of(dom, d)
+                if not (loss == l0 or (loss != loss and l0 != l0)):
+                    return False
         if len(self._pending) <= _PENDING_RECHECK:
             for r in list(self._pending):
                 loss = _loss_of(dom, self.docs[r])
@@ -216,9 +223,11 @@ class TrialHistory(object):
         self._forget()
         self._dev = dev
         best = {}               # tid -> [loss, doc]
+        seen = {}               # id(doc) -> its loss now
         for doc in view:
             tid = doc['misc'].get('from_tid', doc['tid'])
             loss = _loss_of(dom, doc)
+            seen[id(doc)] = loss
             cur = best.get(tid)
             if cur is None:
                 best[tid] = [loss, doc if loss == loss else None]
@@ -227,7 +236,7 @@ class TrialHistory(object):
         rows = sorted(((t, e[0], e[1]) for t, e in best.items() if e[1] is not None),
                       key=lambda z: z[0])
         kept = {id(e[2]) for e in rows}
-        self._dropped = {id(d): d for d in view if id(d) not in kept}
+        self._dropped = {id(d): (d, seen[id(d)]) for d in view if id(d) not in kept}
         self._grow(len(rows))
         plain = True
         for r, (tid, loss, doc) in enumerate(rows):

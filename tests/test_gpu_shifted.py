@@ -426,3 +426,46 @@ def test_config3_categorical_posteriors_bit_exact():
             np.testing.assert_array_equal(w[:t.upper], ref, err_msg='%s side %d' % (h.label, side))
             n_checked += o.size > 1024
     assert n_checked >= 2
+
+
+def test_config5_bench_shape_multichunk_batch_vs_oracle():
+    """Config 5 exactly as ``bench.py --config cfg5`` runs it: config 2's
+    space and history, one fit_suggest of S = 16 suggestions x 1e6
+    candidates.  That exceeds the 2 GB candidate chunk, so the level runs as
+    several chunks whose winners accumulate (ScoreArgs::accumulate), on
+    value-bucketed sorted draws and wave tiles (tpe_engine.hip run_level).
+    The reference serves one id per call (tpe.py:812), so parity is per
+    suggestion: every winner's value is the draw at its reported global
+    index (broadcast_best returns samples[best], tpe.py:756-757), its score
+    is the oracle's lpdf difference at that value (1e-6), and suggestion s
+    equals the single-seed fit_suggest([seed_s], 1e6) (one chunk) byte for
+    byte -- chunk boundaries are multiples of the 4096-candidate sorted-draw
+    block, so no pruned sum depends on the chunking."""
+    import bench
+    dom, losses, vals, act = bench.build_workload('cfg2')
+    hps, conds, pprior = dom.space.engine_tables()
+    plan = E.Plan(E.default_engine(), hps, conds, pprior, max_trials=losses.size)
+    plan.set_history(losses, vals, act)
+    obs = _oracle_obs(dom, losses, vals, act)
+    n, S = 1_000_000, 16
+    seeds = [1_000_003 + 7919 * s for s in range(S)]
+    plan.profile(64)
+    batch = plan.fit_suggest(seeds, n)
+    _, launches, _ = plan.profile_read(0)
+    plan.profile(0)
+    assert launches >= 2, 'the batch ran in %d chunk(s): not the bench shape' % launches
+    dev, orc = [], []
+    for s, sd in enumerate(seeds):
+        assert batch[s]['active'].all()
+        d, o = _check_winners(dom, plan, batch[s], sd, n, obs, 'cfg5 batch s=%d' % s)
+        dev += d
+        orc += o
+    _record('cfg5_batch_winners_vs_oracle', **_delta(dev, orc))
+    for s in (0, 5, S - 1):
+        plan.profile(64)
+        one = plan.fit_suggest([seeds[s]], n)[0]
+        _, l1, _ = plan.profile_read(0)
+        plan.profile(0)
+        assert l1 == 1
+        np.testing.assert_array_equal(one.view(np.uint8), batch[s].view(np.uint8),
+                                      err_msg='suggestion %d: batch vs single' % s)

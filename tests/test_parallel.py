@@ -165,8 +165,9 @@ def _gpu_worker(rank, world, port, outdir, n_cand):
     eng = E.Engine(0)
     plan = E.Plan(eng, hps, conds, pprior, max_trials=losses.size)
     plan.set_history(losses, vals, act)
-    plan.fit()
-    sharded = PAR.ShardedSuggest(plan).suggest([5, 6, 7], n_cand)
+    sh = PAR.ShardedSuggest(plan)
+    sh.fit()  # on the sharded stream: ordered before its suggest
+    sharded = sh.suggest([5, 6, 7], n_cand)
     if rank == 0:
         full = plan.suggest([5, 6, 7], n_cand)
         np.save(os.path.join(outdir, 'full.npy'), full.view(np.uint8))
@@ -176,11 +177,16 @@ def _gpu_worker(rank, world, port, outdir, n_cand):
 
 
 @pytest.mark.gpu
-def test_sharded_suggest_two_ranks_equals_single_device():
+@pytest.mark.parametrize('n_cand', [5000, 24, 4096])
+def test_sharded_suggest_two_ranks_equals_single_device(n_cand):
+    """Two ranks on one GPU equal one device.  24 and 4096 candidates leave
+    rank 1 an empty shard (4096-aligned shards): its records must say
+    "nothing here" (NaN, -1, inactive) and not leak a previous suggest's
+    winners into the merge (tpe.py:750-759: no samples, no value)."""
     import torch.multiprocessing as mp
     port = _free_port()
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_gpu_worker, args=(2, port, d, 5000), nprocs=2, join=True)
+        mp.spawn(_gpu_worker, args=(2, port, d, n_cand), nprocs=2, join=True)
         full = np.load(os.path.join(d, 'full.npy')).view(RESULT_DTYPE)
         for r in range(2):
             got = np.load(os.path.join(d, 'r%d.npy' % r)).view(RESULT_DTYPE)
@@ -203,8 +209,9 @@ def _gpu_worker_cfg4(rank, world, port, outdir, n_cand):
     hps, conds, pprior = dom.space.engine_tables()
     plan = E.Plan(E.Engine(0), hps, conds, pprior, max_trials=losses.size)
     plan.set_history(losses, vals, act)
-    plan.fit()
-    sharded = PAR.ShardedSuggest(plan).suggest([7], n_cand)
+    sh = PAR.ShardedSuggest(plan)
+    sh.fit()  # on the sharded stream: ordered before its suggest
+    sharded = sh.suggest([7], n_cand)
     if rank == 0:
         full = plan.suggest([7], n_cand)
         np.save(os.path.join(outdir, 'full.npy'), full.view(np.uint8))
@@ -254,9 +261,10 @@ def _nccl_worker(rank, world, port, outdir):
     hps, conds, pprior = dom.space.engine_tables()
     plan = E.Plan(E.Engine(0), hps, conds, pprior, max_trials=losses.size)
     plan.set_history(losses, vals, act)
-    plan.fit()
     assert dist.get_backend() == 'nccl'
-    got = PAR.ShardedSuggest(plan).suggest([5, 6], 3000)
+    sh = PAR.ShardedSuggest(plan)
+    sh.fit()
+    got = sh.suggest([5, 6], 3000)
     full = plan.suggest([5, 6], 3000)
     np.save(os.path.join(outdir, 'got.npy'), got.view(np.uint8))
     np.save(os.path.join(outdir, 'full.npy'), full.view(np.uint8))

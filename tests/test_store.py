@@ -332,3 +332,23 @@ def test_dropped_document_reassigned_enters_history():
     t.trials[1]['result'] = {'status': 'ok', 'loss': 0.25}
     check(dom, t, hist, plan)
     assert hist.tids == [0, 1, 2, 3]
+
+
+def test_dropped_document_mutated_in_place_enters_history():
+    """the same document's loss changed in place
+    (doc['result']['loss'] = x, no journal entry) also enters the history:
+    the few dropped documents' losses are re-read on every sync."""
+    dom = Domain(lambda x: 0, SPACE)
+    t = Trials()
+    hist = TrialHistory(dom)
+    plan = FakePlan(len(dom.space.labels), 64)
+    t.insert_trial_docs(rand.suggest([0, 1, 2], dom, t, 5))
+    t.refresh()
+    for i, d in enumerate(t.trials):
+        d['result'] = {'status': 'ok', 'loss': float('nan') if i == 1 else float(i)}
+        d['state'] = H.JOB_STATE_DONE
+    check(dom, t, hist, plan)
+    assert hist.tids == [0, 2]
+    t.trials[1]['result']['loss'] = 0.25          # in place: no journal entry
+    check(dom, t, hist, plan)
+    assert hist.tids == [0, 1, 2]
