@@ -77,6 +77,9 @@ class CompiledSpace(object):
         for i, h in enumerate(self.hps):
             h.index = i
         self.by_label = {h.label: h for h in self.hps}
+        # (label, engine index, categorical?) of every hp: tpe.suggest's
+        # record -> value conversion
+        self.pick_order = [(h.label, h.index, h.is_categorical) for h in self.hps]
         self.draw_order = self._draw_order()
         self._engine_tables = None
 

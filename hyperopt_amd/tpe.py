@@ -37,7 +37,6 @@ import numpy as np
 
 from . import _engine as E
 from . import rand, rstream
-from .base import miscs_update_idxs_vals
 from .history import TrialHistory
 
 logger = logging.getLogger(__name__)
@@ -119,11 +118,29 @@ def _fmt(h, v):
 
 
 def _new_doc(domain, trials, cs, new_id, chosen):
-    idxs = {lab: ([new_id] if lab in chosen else []) for lab in cs.labels}
-    vls = {lab: ([chosen[lab]] if lab in chosen else []) for lab in cs.labels}
-    misc = dict(tid=new_id, cmd=domain.cmd, workdir=domain.workdir)
-    miscs_update_idxs_vals([misc], idxs, vls)
+    """The returned document (tpe.py:887-897): misc idxs / vals of the one
+    new id -- what miscs_update_idxs_vals(idxs_map={fake_ids[0]: new_id})
+    leaves in it, built directly (one misc, every label present)."""
+    misc = dict(tid=new_id, cmd=domain.cmd, workdir=domain.workdir,
+                idxs={lab: ([new_id] if lab in chosen else []) for lab in cs.labels},
+                vals={lab: ([chosen[lab]] if lab in chosen else []) for lab in cs.labels})
     return trials.new_trial_docs([new_id], [None], [domain.new_result()], [misc])[0]
+
+
+def _picks(cs, res):
+    """{label: value} of every suggestion's active winners, from the engine's
+    [S][P] records (one conversion to Python lists, no per-field numpy
+    scalar access)."""
+    S = res.shape[0]
+    act = res['active'].tolist()
+    idx = res['index'].tolist()
+    val = res['value'].tolist()
+    out = []
+    for s in range(S):
+        a, i, v = act[s], idx[s], val[s]
+        out.append({lab: (int(round(v[j])) if cat else v[j])
+                    for lab, j, cat in cs.pick_order if a[j] and i[j] >= 0})
+    return out
 
 
 def suggest(new_ids, domain, trials, seed,
@@ -163,14 +180,7 @@ def suggest(new_ids, domain, trials, seed,
             # fit + sample + score + argmax of every suggestion in one call
             res = plan.fit_suggest(seeds, n_ei, gamma=gamma, prior_weight=prior_weight,
                                    lf=DEFAULT_LF)
-            picks = []
-            for s in range(len(new_ids)):
-                chosen = {}
-                for h in cs.hps:
-                    r = res[s, h.index]
-                    if r['active'] and r['index'] >= 0:
-                        chosen[h.label] = _fmt(h, r['value'])
-                picks.append(chosen)
+            picks = _picks(cs, res)
         else:
             plan.fit(gamma=gamma, prior_weight=prior_weight, lf=DEFAULT_LF)
             picks = [_suggest_numpy_stream(cs, plan, sd, n_ei) for sd in seeds]
