@@ -445,7 +445,7 @@ def main():
     plan.census(True)
     for i in range(n_prof):
         step(args.warmup + args.steps + n_prof + i)
-    census = plan.census(False)
+    census = plan.census(False, n=9)
 
     e2e = None
     if rank == 0 and world == 1 and not args.no_e2e:
@@ -522,6 +522,8 @@ def report(args, C, eng, world, mode, elapsed, value, pairs_step, pairs_suggest,
                      'pair below the one-exponent size: the same in fp32 with the group max and '
                      'lift; quantized pair: 2 OCML fp64 erf + 8 flops)',
                 lse_evaluated_shifted_pairs_per_launch=lse_shift,
+                lse_shifted_retry_pairs_per_launch=census[7] / per_launch,
+                lse_shifted_wide_block_pairs_per_launch=census[8] / per_launch,
                 lse_evaluated_exact_f32_pairs_per_launch=lse_exact32,
                 lse_pair_max_lift_f32_peak_per_s=lse_peak_exact32,
                 lse_pairs_per_launch=lse_pairs, lse_evaluated_pairs_per_launch=lse_exec,

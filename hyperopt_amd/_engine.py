@@ -532,16 +532,18 @@ class Plan(object):
         with e.lock:
             e.check(e.lib.tpe_plan_set_prune(self.p, mode))
 
-    def census(self, enable):
+    def census(self, enable, n=7):
         """Pair census since the last call: (quantized total, live, evaluated,
         log-sum-exp total, log-sum-exp evaluated in the one-exponent form,
-        log-sum-exp evaluated, of those in the fp32 per-group-lift form);
-        enable it for the following suggests."""
+        log-sum-exp evaluated, of those in the fp32 per-group-lift form[,
+        one-exponent pairs re-evaluated by a wave's second attempt,
+        one-exponent pairs of wide blocks (mode 3's fp64 loop)]) -- the first
+        ``n`` (7 or 9); enable it for the following suggests."""
         e = self.engine
-        out = (C.c_int64 * 7)()
+        out = (C.c_int64 * 9)()
         with e.lock:
-            e.check(e.lib.tpe_plan_census_n(self.p, int(bool(enable)), out, 7))
-        return tuple(int(v) for v in out)
+            e.check(e.lib.tpe_plan_census_n(self.p, int(bool(enable)), out, int(n)))
+        return tuple(int(v) for v in out[:n])
 
     def last_stats(self):
         e = self.engine

@@ -19,11 +19,6 @@
 using namespace tpe;
 
 static int lse_shift_min();
-static bool compact_on();
-static bool lat_side_on();
-static bool cat_counting_on();
-static bool sort_by_rows();
-static bool wave_tiles_on();
 static bool small_sort_on();
 static int64_t chunk_budget();
 constexpr int64_t kSmallSortMin = 2048;  // candidates per chunk worth bucketing a small draw
@@ -565,7 +560,6 @@ FitArgs fit_args(tpe_plan *p, int32_t n_below, double prior_weight, int32_t lf) 
   a.ld = p->ncap;
   a.n_below = n_below;
   a.lf = lf;
-  a.cat_counting = cat_counting_on() ? 1 : 0;
   a.prior_weight = prior_weight;
   a.pprior = p->d_pprior;
   a.mw = p->d_mw;
@@ -643,7 +637,7 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
   // choice cost no blocks
   const int32_t *hl = p->levels[level].data();
   const int32_t lvl_rows = active_bound(p, hl, 0, n_level);
-  const bool compact = compact_on() && lvl_rows < n_level;
+  const bool compact = lvl_rows < n_level;
   const int32_t slot_rows = compact ? lvl_rows : n_level;
   const int32_t lat_rows =
       compact ? (int32_t)std::min<int64_t>(n_lat, n_sug * (int64_t)active_bound(p, hl, 0, n_lat))
@@ -672,7 +666,7 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
   // (fuse_draw), it runs on a side stream beside the candidate draw (fork /
   // join events; a parallel branch of the captured graph), and the scoring
   // launch waits for it
-  const bool lat_side = lat_level && !fuse_draw && lat_side_on();
+  const bool lat_side = lat_level && !fuse_draw;
   if (lat_level && !fuse_draw) {
     ScoreArgs la = base_args(p, n_sug);
     la.level_hps = lvl;
@@ -727,7 +721,7 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
     // tiles then skip the component blocks that are exact zeros for them,
     // on wave tiles when the wave-wide exponent is on (prune mode 2)
     const bool sorted_draw = !fuse_draw && table_draw &&
-                             cn * n_sug * (sort_by_rows() ? slot_rows : n_level) >= ((int64_t)1 << 22);
+                             cn * n_sug * n_level >= ((int64_t)1 << 22);
     // small draws of >= kSmallSortMin candidates: the log-sum-exp slots are
     // value-bucketed too (k_bucket, stable, <= 8192 per bucketing chunk) and
     // pruned on the 8-wave tiles
@@ -736,7 +730,13 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
       for (int k : kinds) small_sort |= k == KIND_LSE_G || k == KIND_LSE_L || k == KIND_LSE_G1 ||
                                         k == KIND_LSE_L1;
     std::vector<int> ck(kinds);
-    if (sorted_draw && p->prune_mode > 1 && wave_tiles_on())
+    if (sorted_draw && p->prune_mode > 1)
+      // pruned log-sum-exp slots on wave tiles: each wave its own 128
+      // candidates and every live block, so its one exponent and its accuracy
+      // guard see the whole sum.  (Round 4, config 3: 8-wave component-split
+      // tiles below 2^18 candidates measured 0.265 ms with the one-exponent
+      // form -- a wave's guard sees 1/8 of the components and 3e7 pairs per
+      // launch were retried -- and 0.236 ms without it, against 0.234 ms here.)
       for (int &k : ck)
         k = (k == KIND_LSE_G || k == KIND_LSE_G1) ? KIND_LSE_GW
           : (k == KIND_LSE_L || k == KIND_LSE_L1) ? KIND_LSE_LW : k;
@@ -774,6 +774,10 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
     a.lse_pos = (sorted_draw || small_sort) ? 1 : 0;
     a.lse_prune = (sorted_draw || small_sort) ? p->prune_mode : 0;
     a.lse_shift_min = lse_shift_min();
+    // prune mode 3's block-local fp32 pairs on every log-sum-exp slot of the
+    // suggest, pruned (large draws) or not (small draws: every pair, 8-wave
+    // component-split tiles)
+    a.lse_f32 = p->prune_mode == 3 ? 1 : 0;
     if (fuse_draw) {
       tpe_plan::Prof *pr = nullptr;
       if (p->prof_cap > 0 && p->prof[1].n < p->prof_cap) pr = &p->prof[1];
@@ -819,7 +823,7 @@ int run_external(tpe_engine *h, tpe_plan *p, int32_t hp, const double *ext, int6
                  double *lb, double *la, hipStream_t st, int32_t sorted_mode = -1) {
   int kind = score_kind(p->hps[hp]);
   const bool sorted = sorted_mode >= 0;
-  if (sorted && sorted_mode > 1 && wave_tiles_on())
+  if (sorted && sorted_mode > 1)
     kind = kind == KIND_LSE_G ? KIND_LSE_GW : kind == KIND_LSE_L ? KIND_LSE_LW : kind;
   ScoreArgs grid{};
   const int32_t pstride = set_score_groups(grid, &kind, 1, n);
@@ -1657,56 +1661,10 @@ int tpe_plan_sample_prior(tpe_plan_t p, const uint64_t *seeds, int64_t n_sug, tp
   return copy_results(h, p, n_sug, out, out_on_device, st);
 }
 
-// lse_prune mode 2's smallest mixture (TPE_SHIFT_MIN_K overrides; tuning)
-// log-sum-exp wave tiles on the pruned path (TPE_WAVE_TILES=0: 8-wave
-// component-split tiles everywhere, for A/B measurements)
-static bool wave_tiles_on() {
-  static const bool v = [] {
-    const char *e = std::getenv("TPE_WAVE_TILES");
-    return !(e && std::atoi(e) == 0);
-  }();
-  return v;
-}
-
 // value-bucketed, pruned log-sum-exp slots on small draws: opt-in
-// (TPE_SMALL_SORT=1).  Measured at config 2 (4096 candidates): the skip drops
-// 80 % of the pairs and k_score from 33 to 23 us, but the extra k_bucket
-// launch costs more than that (suggest 70 -> 78 us)
-// compact (active-slot) grids of conditional levels; TPE_COMPACT=0 turns
-// them off (A/B measurements)
-static bool cat_counting_on() {  // TPE_CAT_COUNT=0: categorical fits always sort
-  static const bool on = [] {
-    const char *e = std::getenv("TPE_CAT_COUNT");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
-static bool lat_side_on() {  // TPE_LAT_SIDE=0: the lattice on the main stream
-  static const bool on = [] {
-    const char *e = std::getenv("TPE_LAT_SIDE");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
-static bool compact_on() {
-  static const bool on = [] {
-    const char *e = std::getenv("TPE_COMPACT");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-// the large-draw (value-bucketed) path is picked by the draws of the hps
-// that can be active (TPE_SORT_ROWS=1) instead of every hp of the level
-static bool sort_by_rows() {
-  static const bool on = [] {
-    const char *e = std::getenv("TPE_SORT_ROWS");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
+// (TPE_SMALL_SORT=1, test_gpu_suggest.py).  Measured at config 2 (4096
+// candidates): the skip drops 80 % of the pairs and k_score from 33 to 23 us,
+// but the extra k_bucket launch costs more than that (suggest 70 -> 78 us)
 static bool small_sort_on() {
   static const bool v = [] {
     const char *e = std::getenv("TPE_SMALL_SORT");
@@ -1724,10 +1682,16 @@ static int64_t chunk_budget() {
   return v;
 }
 
+// smallest mixture (components) scored in the one-exponent form on pruned
+// tiles; smaller ones keep the per-group lift (TPE_SHIFT_MIN_K overrides:
+// A/B and tests).  Round 4: 2048 -> 512 -- config 5 (K_a = 993) 997 -> 885
+// ms per 1024-suggestion step, config 3 (K_a ~ 1.4e3) 0.266 -> 0.255 ms;
+// below ~128 components (the good-side mixtures) the guard's second attempt
+// costs more than the lift saves (0: config 5 905 ms)
 static int lse_shift_min() {
   static const int v = [] {
     const char *e = std::getenv("TPE_SHIFT_MIN_K");
-    return e ? std::atoi(e) : 2048;
+    return e ? std::atoi(e) : 512;
   }();
   return v;
 }

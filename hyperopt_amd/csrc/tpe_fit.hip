@@ -1264,7 +1264,7 @@ __device__ __forceinline__ void fit_slot(const FitArgs &A, unsigned char *dyn_ld
   if constexpr (!SMALL) {
     // categorical over few bins, more observations than the merge sort's:
     // no sort (fit_categorical_counting)
-    if (lds_sort && cat && H.upper <= kCatFastBins && m > kMergeMax && A.cat_counting) {
+    if (lds_sort && cat && H.upper <= kCatFastBins && m > kMergeMax) {
       STAMP(3);
       fit_categorical_counting(A, C, sm, H, slot, m);
       done = true;

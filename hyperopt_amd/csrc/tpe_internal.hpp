@@ -89,8 +89,10 @@ struct MixInfo {
 constexpr float kLseDeadBase = 30.0f;
 // census counters (tpe_plan_census_n): quantized total / live / evaluated,
 // log-sum-exp total / one-exponent evaluated / evaluated / evaluated in the
-// block-local fp32 per-group-lift form
-constexpr int kCensus = 7;
+// block-local fp32 per-group-lift form / one-exponent pairs of a wave's
+// second attempt (re-centred exponent) / one-exponent pairs of wide blocks
+// (the fp64 loop of mode 3)
+constexpr int kCensus = 9;
 
 // Per-component scoring coefficients (make_coef, tpe_device.hpp), 4 fields:
 //   LSE: x = alpha, y = beta, z = gamma (t = alpha + y'(beta + gamma y'))
@@ -212,6 +214,8 @@ struct ScoreArgs {
   int32_t lse_pos;           // LSE slots' candidates are value-bucketed (cand_pos valid)
   int32_t lse_prune;         // skip log-sum-exp blocks of exact-zero terms (needs lse_pos)
   int32_t lse_shift_min;     // lse_prune 2: smallest mixture (components) for one wave exponent
+  int32_t lse_f32;           // unpruned log-sum-exp slots also take the block-local fp32
+                             // pairs (prune mode 3's arithmetic on small draws)
   const LatInfo *lat_info;   // [P] value lattices (KIND_LAT slots)
   const double2 *lat;        // lattice (lpdf below, lpdf above) pairs
 };
@@ -226,7 +230,6 @@ struct FitArgs {
   int64_t ld;                // row stride of vals / active (the plan's trial capacity)
   int32_t n_below;
   int32_t lf;
-  int32_t cat_counting;      // categorical fits of > 1024 observations without the sort
   int32_t pad0;
   double prior_weight;
   const double *pprior;

@@ -392,9 +392,9 @@ __global__ __launch_bounds__(256) void k_micro(int iters, double *sink) {
     if (acc == 12345.0) sink[t] = acc;
   } else if constexpr (WHICH == 6) {
     // one log-sum-exp pair of prune mode 3 (lse_terms_f32): u = fp32(y' -
-    // centre) once per (candidate, block), (A - M) + alpha per component,
-    // two packed fp32 FMAs per component pair, exp2, fp32 tree, fp64 sum;
-    // 4 candidates x 8 components
+    // centre) and u^2 once per (candidate, block), (A - M) + alpha per
+    // component, two packed fp32 FMAs per component pair (gamma u^2 + (beta u
+    // + alpha')), exp2, fp32 tree, fp64 sum; 4 candidates x 8 components
     typedef float f2v __attribute__((ext_vector_type(2)));
     double y[4], sm[4];
 #pragma unroll
@@ -412,11 +412,12 @@ __global__ __launch_bounds__(256) void k_micro(int iters, double *sink) {
       for (int c = 0; c < 4; ++c) {
         const float u = (float)(y[c] - centre);
         const f2v u2 = {u, u};
+        const f2v uu2 = u2 * u2;
         float e[8];
 #pragma unroll
         for (int k = 0; k < 8; k += 2) {
           const f2v a2 = {ca[k], ca[k + 1]}, b2 = {cb[k], cb[k + 1]}, c2 = {cc[k], cc[k + 1]};
-          const f2v z = __builtin_elementwise_fma(__builtin_elementwise_fma(c2, u2, b2), u2, a2 + am2);
+          const f2v z = __builtin_elementwise_fma(c2, uu2, __builtin_elementwise_fma(b2, u2, a2 + am2));
           e[k] = __builtin_amdgcn_exp2f(z.x);
           e[k + 1] = __builtin_amdgcn_exp2f(z.y);
         }
@@ -565,14 +566,6 @@ hipError_t launch_draw(const ScoreArgs &a, bool table, hipStream_t st) {
   return hipGetLastError();
 }
 
-static bool wide_draw_on() {  // TPE_WIDE_DRAW=0: always 256-thread sorted-draw blocks
-  static const bool on = [] {
-    const char *e = std::getenv("TPE_WIDE_DRAW");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 hipError_t launch_draw_sorted(const ScoreArgs &a, bool small_table, int32_t *pos_out,
                               hipStream_t st) {
   if (a.n_slots <= 0 || a.n_suggest <= 0 || a.n_cand <= 0) return hipSuccess;
@@ -580,7 +573,7 @@ hipError_t launch_draw_sorted(const ScoreArgs &a, bool small_table, int32_t *pos
   const dim3 g(gx, (unsigned)a.slot_rows, a.n_suggest);
   // fewer blocks than ~2 per CU: 1024-thread blocks (a 256-thread block is 1
   // wave per SIMD; the launch is then bound by one block's latency)
-  const bool wide = (int64_t)gx * a.slot_rows * a.n_suggest <= 2 * kNumCUs && wide_draw_on();
+  const bool wide = (int64_t)gx * a.slot_rows * a.n_suggest <= 2 * kNumCUs;
   if (wide) {
     if (small_table) k_draw_sorted_wide<kFuseTab><<<g, kWideDrawThreads, 0, st>>>(a, pos_out);
     else k_draw_sorted_wide<kTabCap><<<g, kWideDrawThreads, 0, st>>>(a, pos_out);

@@ -89,7 +89,7 @@ struct CoefGroup {
 // three 64-B scalar loads: the x, y, z rows of the table block at k (whole
 // blocks are allocated, entries past the mixture are masked by the caller)
 __device__ __forceinline__ void load_group(KDbl *__restrict__ cs, int k, CoefGroup &g) {
-  KDbl *b = cs + coef_off(k, 0);
+  KDbl *b = cs + (((unsigned)k >> 3) << 5);  // k >= 0: coef_off(k, 0) of a block start
 #pragma unroll
   for (int j = 0; j < kGroup; ++j) {
     g.x[j] = b[j];
@@ -114,7 +114,8 @@ struct CoefGroup32 {
 };
 // two 64-B scalar loads: the block of component k
 __device__ __forceinline__ void load_group32(KC32 *__restrict__ t, int k, CoefGroup32 &g) {
-  KC32 *b = t + k / kCoefBlock;
+  KC32 *b = t + ((unsigned)k >> 3);  // k >= 0: block k / kCoefBlock
+  static_assert(kCoefBlock == 8, "block shift");
   g.m = b->center;
   g.A = b->base;
 #pragma unroll
@@ -175,17 +176,22 @@ __device__ __forceinline__ void lse_fold(const double (&t)[KR][kGroup], double (
   }
 }
 
-// the next live block of a round (chunk j's block 0 before its block 1
-// before chunk j + 1): its first component, popped from the masks
+// Envelope rounds: the wave's chunks c = c0 (mod STRIDE) in increasing order,
+// 32 chunks (64 blocks of kGroup components) per round, lane l testing block
+// l of the round -- block (l & 1) of chunk r0 + STRIDE (l >> 1) -- so one
+// ballot lists the round's live blocks in evaluation order (chunk j's block 0
+// before its block 1 before chunk j + 1) and the next one is one bit scan.
 template <int STRIDE>
-__device__ __forceinline__ bool next_live(uint64_t &m0, uint64_t &m1, int r0, int &kg) {
-  if (!(m0 | m1)) return false;
-  const int j0 = m0 ? __builtin_ctzll(m0) : 64, j1 = m1 ? __builtin_ctzll(m1) : 64;
-  const int g = j1 < j0 ? 1 : 0;
-  const int j = g ? j1 : j0;
-  if (g) m1 &= m1 - 1;
-  else m0 &= m0 - 1;
-  kg = (r0 + STRIDE * j) * kChunk + g * kGroup;
+__device__ __forceinline__ int round_k(int r0, int j) {
+  return ((r0 + STRIDE * (j >> 1)) * 2 + (j & 1)) * kGroup;
+}
+// the next live block of a round: its first component, popped from the mask
+template <int STRIDE>
+__device__ __forceinline__ bool next_live(uint64_t &m, int r0, int &kg) {
+  if (!m) return false;
+  const int j = __builtin_ctzll(m);
+  m &= m - 1;
+  kg = round_k<STRIDE>(r0, j);
   return true;
 }
 
@@ -201,6 +207,8 @@ struct LseWindow {
 struct LseCensus {
   uint32_t total, exec, shift;  // shift: the evaluated ones in the one-exponent form
   uint32_t f32;                 // the evaluated ones in the fp32 per-group-lift form
+  uint32_t retry;               // one-exponent pairs evaluated again by a second attempt
+  uint32_t wide;                // one-exponent pairs of wide blocks (fp64 loop, mode 3)
 };
 
 // A block's envelope bound over the wave's candidate range [lo, hi]: the
@@ -210,12 +218,12 @@ __device__ __forceinline__ float envelope_bound(const float4 e, const LseWindow 
   return fmaf(-fabsf(e.w), d * d, e.z);  // (the sign of e.w flags a wide block, Coef32)
 }
 
-// The wave's chunks c = c0 (mod kWaves) of a mixture of nb components, in
-// increasing order, 64 chunks per round: lane l first tests the two blocks
-// of chunk c0 + kWaves * (64 r + l) against the window (one vector load of
-// their envelopes, tpe_internal.hpp kLseDeadBase), a ballot gives the round's
-// live blocks, and only those are evaluated, in the same order as the full
-// loop.  prune = false: every block is live.
+// The wave's chunks c = c0 (mod STRIDE) of a mixture of nb components, in
+// increasing order, one envelope round (round_k: 64 blocks) at a time: lane l
+// tests block l of the round against the window (one vector load of its
+// envelope, tpe_internal.hpp kLseDeadBase), a ballot gives the round's live
+// blocks, and only those are evaluated, in the same order as the full loop.
+// prune = false: every block is live.
 // The same fold from the block-local fp32 form (prune mode 3, Coef32, blocks
 // that are not wide): z = t - A by two packed fp32 FMAs per component pair
 // (lse_terms_z, before the next block's coefficients are loaded), then the
@@ -282,25 +290,19 @@ __device__ __forceinline__ void lse_chunks(KDbl *__restrict__ cs, const Coef *__
 #pragma unroll
   for (int r = 0; r < KR; ++r) { m[r] = -INFINITY; s[r] = 0.0; y2[r] = y[r] * y[r]; }
   const int nch = (nb + kChunk - 1) / kChunk;
-  for (int r0 = c0; r0 < nch; r0 += STRIDE * 64) {
-    const int c = r0 + STRIDE * lane;
-    const int k0 = c * kChunk;
-    const bool has0 = c < nch, has1 = has0 && k0 + kGroup < nb;
-    bool live0 = has0, live1 = has1, wide0 = false, wide1 = false;
-    if ((prune || F32) && has0) {
+  for (int r0 = c0; r0 < nch; r0 += STRIDE * 32) {
+    const int k0 = round_k<STRIDE>(r0, lane);
+    const bool has = r0 + STRIDE * (lane >> 1) < nch && k0 < nb;
+    bool live = has, wide = false;
+    if ((prune || F32) && has) {
       const double *t = reinterpret_cast<const double *>(cv);
-      const float4 e0 = *reinterpret_cast<const float4 *>(t + coef_off(k0, 3));
-      if (prune) live0 = envelope_bound(e0, win) >= win.thr;
-      wide0 = __builtin_signbit(e0.w);
-      if (has1) {
-        const float4 e1 = *reinterpret_cast<const float4 *>(t + coef_off(k0 + kGroup, 3));
-        if (prune) live1 = envelope_bound(e1, win) >= win.thr;
-        wide1 = __builtin_signbit(e1.w);
-      }
+      const float4 e = *reinterpret_cast<const float4 *>(t + coef_off(k0, 3));
+      if (prune) live = envelope_bound(e, win) >= win.thr;
+      wide = __builtin_signbit(e.w);
     }
     if constexpr (CENSUS) {
-      const int n0 = has0 ? min(kGroup, nb - k0) : 0, n1 = has1 ? min(kGroup, nb - k0 - kGroup) : 0;
-      uint32_t tot = (uint32_t)(n0 + n1), ex = (uint32_t)((live0 ? n0 : 0) + (live1 ? n1 : 0));
+      const int n = has ? min(kGroup, nb - k0) : 0;
+      uint32_t tot = (uint32_t)n, ex = (uint32_t)(live ? n : 0);
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) {
         tot += __shfl_xor(tot, o, 64);
@@ -309,22 +311,21 @@ __device__ __forceinline__ void lse_chunks(KDbl *__restrict__ cs, const Coef *__
       cen.total += tot * (uint32_t)nvalid;
       cen.exec += ex * (uint32_t)nvalid;
       if constexpr (F32) {
-        uint32_t fx = (uint32_t)((live0 && !wide0 ? n0 : 0) + (live1 && !wide1 ? n1 : 0));
+        uint32_t fx = (uint32_t)(live && !wide ? n : 0);
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) fx += __shfl_xor(fx, o, 64);
         cen.f32 += fx * (uint32_t)nvalid;
       }
     }
-    uint64_t m0 = __ballot(live0 && !(F32 && wide0)), m1 = __ballot(live1 && !(F32 && wide1));
-    // live blocks in order: chunk j's block 0 before its block 1 before chunk
-    // j + 1 (the padding components of a last block have alpha = -inf,
-    // make_coef_pad, so no tail masking is needed)
+    uint64_t mk = __ballot(live && !(F32 && wide));
+    // live blocks in order (the padding components of a last block have
+    // alpha = -inf, make_coef_pad, so no tail masking is needed);
     // software-pipelined: the next live block's coefficients are loaded into
     // the same scalar registers once this block's terms are formed, so the
     // load overlaps the block's max / exp / sum (scalar loads complete out of
     // order, so only one batch may be in flight)
     int kg = 0;
-    bool have = next_live<STRIDE>(m0, m1, r0, kg);
+    bool have = next_live<STRIDE>(mk, r0, kg);
     if constexpr (F32) {
       CoefGroup32 g32;
       if (have) load_group32(c32, kg, g32);
@@ -332,13 +333,13 @@ __device__ __forceinline__ void lse_chunks(KDbl *__restrict__ cs, const Coef *__
         float z[KR][kGroup];
         lse_terms_z<KR>(g32, y, z);
         const float A = g32.A;
-        have = next_live<STRIDE>(m0, m1, r0, kg);
+        have = next_live<STRIDE>(mk, r0, kg);
         load_group32(c32, kg, g32);
         __builtin_amdgcn_sched_barrier(0);
         lse_fold_z<KR>(z, A, m, s);
       }
-      uint64_t x0 = __ballot(live0 && wide0), x1 = __ballot(live1 && wide1);
-      while (next_live<STRIDE>(x0, x1, r0, kg)) {
+      uint64_t xk = __ballot(live && wide);
+      while (next_live<STRIDE>(xk, r0, kg)) {
         CoefGroup g;
         load_group(cs, kg, g);
         double t[KR][kGroup];
@@ -351,7 +352,7 @@ __device__ __forceinline__ void lse_chunks(KDbl *__restrict__ cs, const Coef *__
       while (have) {
         double t[KR][kGroup];
         lse_terms<KR>(cgp, y, y2, t);
-        have = next_live<STRIDE>(m0, m1, r0, kg);  // (kg kept after the last)
+        have = next_live<STRIDE>(mk, r0, kg);  // (kg kept after the last)
         load_group(cs, kg, cgp);  // unconditional: no branch merge of the registers
         __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of the fold
         lse_fold<KR>(t, m, s);
@@ -408,6 +409,20 @@ __device__ __forceinline__ void lse_fold_shifted(const float (&d)[KR][kGroup], d
     s[r] += (double)(t0 + t1);
   }
 }
+// the same block's terms summed in fp32 only (bs), for a caller that adds two
+// blocks' sums in fp32 before the fp64 accumulation
+template <int KR>
+__device__ __forceinline__ void lse_block_sum(const float (&d)[KR][kGroup], float (&bs)[KR]) {
+#pragma unroll
+  for (int r = 0; r < KR; ++r) {
+    float e[kGroup];
+#pragma unroll
+    for (int j = 0; j < kGroup; ++j) e[j] = __builtin_amdgcn_exp2f(d[r][j]);
+    const float t0 = (e[0] + e[2]) + (e[1] + e[3]);
+    const float t1 = (e[4] + e[6]) + (e[5] + e[7]);
+    bs[r] = t0 + t1;
+  }
+}
 
 // Mode 3: t - M of the block in fp32, u = fp32(y' - center) once per
 // (candidate, block), then t - M = fma(fma(gamma, u, beta), u, (A - M) +
@@ -420,15 +435,24 @@ __device__ __forceinline__ void lse_fold_shifted(const float (&d)[KR][kGroup], d
 template <int KR>
 __device__ __forceinline__ void lse_terms_f32(const CoefGroup32 &g, float Mf,
                                               const double (&y)[KR], float (&d)[KR][kGroup]) {
+  // t - M = gamma u^2 + (beta u + (alpha + (A - M))): each packed FMA reads
+  // one scalar (SGPR) coefficient pair -- alpha + (A - M) is formed once per
+  // block in VGPRs and shared by the rows, u^2 once per row -- so no VALU
+  // move of a second coefficient pair is needed (one scalar operand per VOP3P)
   const float am = g.A - Mf;
+  const f2v am2 = {am, am};
+  f2v a2m[kGroup / 2];
+#pragma unroll
+  for (int j = 0; j < kGroup; j += 2) a2m[j / 2] = f2v{g.a[j], g.a[j + 1]} + am2;
 #pragma unroll
   for (int r = 0; r < KR; ++r) {
     const float u = (float)(y[r] - g.m);
-    const f2v u2 = {u, u}, am2 = {am, am};
+    const f2v u2 = {u, u};
+    const f2v uu2 = u2 * u2;
 #pragma unroll
     for (int j = 0; j < kGroup; j += 2) {
-      const f2v a2 = {g.a[j], g.a[j + 1]}, b2 = {g.b[j], g.b[j + 1]}, c2 = {g.c[j], g.c[j + 1]};
-      const f2v t = __builtin_elementwise_fma(__builtin_elementwise_fma(c2, u2, b2), u2, a2 + am2);
+      const f2v b2 = {g.b[j], g.b[j + 1]}, c2 = {g.c[j], g.c[j + 1]};
+      const f2v t = __builtin_elementwise_fma(c2, uu2, __builtin_elementwise_fma(b2, u2, a2m[j / 2]));
       d[r][j] = t.x;
       d[r][j + 1] = t.y;
     }
@@ -447,17 +471,11 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
   // pass 1: the largest live block bound of the wave's chunks, and the block
   float bmax = -INFINITY;
   int barg = -1;
-  for (int r0 = c0; r0 < nch; r0 += STRIDE * 64) {
-    const int c = r0 + STRIDE * lane;
-    const int k0 = c * kChunk;
-    if (c < nch) {
-      const float b0 = envelope_bound(*reinterpret_cast<const float4 *>(tb + coef_off(k0, 3)), win);
-      if (b0 >= win.thr && b0 > bmax) { bmax = b0; barg = k0; }
-      if (k0 + kGroup < nb) {
-        const float b1 =
-            envelope_bound(*reinterpret_cast<const float4 *>(tb + coef_off(k0 + kGroup, 3)), win);
-        if (b1 >= win.thr && b1 > bmax) { bmax = b1; barg = k0 + kGroup; }
-      }
+  for (int r0 = c0; r0 < nch; r0 += STRIDE * 32) {
+    const int k0 = round_k<STRIDE>(r0, lane);
+    if (r0 + STRIDE * (lane >> 1) < nch && k0 < nb) {
+      const float b = envelope_bound(*reinterpret_cast<const float4 *>(tb + coef_off(k0, 3)), win);
+      if (b >= win.thr && b > bmax) { bmax = b; barg = k0; }
     }
   }
   float wmax = bmax;
@@ -504,25 +522,18 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
   for (int attempt = 0;; ++attempt) {
 #pragma unroll
     for (int r = 0; r < KR; ++r) s[r] = 0.0;
-    for (int r0 = c0; r0 < nch; r0 += STRIDE * 64) {
-      const int c = r0 + STRIDE * lane;
-      const int k0 = c * kChunk;
-      const bool has0 = c < nch, has1 = has0 && k0 + kGroup < nb;
-      bool live0 = false, live1 = false, wide0 = false, wide1 = false;
-      if (has0) {
-        const float4 e0 = *reinterpret_cast<const float4 *>(tb + coef_off(k0, 3));
-        live0 = envelope_bound(e0, win) >= win.thr;
-        wide0 = __builtin_signbit(e0.w);
-        if (has1) {
-          const float4 e1 = *reinterpret_cast<const float4 *>(tb + coef_off(k0 + kGroup, 3));
-          live1 = envelope_bound(e1, win) >= win.thr;
-          wide1 = __builtin_signbit(e1.w);
-        }
+    for (int r0 = c0; r0 < nch; r0 += STRIDE * 32) {
+      const int k0 = round_k<STRIDE>(r0, lane);
+      const bool has = r0 + STRIDE * (lane >> 1) < nch && k0 < nb;
+      bool live = false, wide = false;
+      if (has) {
+        const float4 e = *reinterpret_cast<const float4 *>(tb + coef_off(k0, 3));
+        live = envelope_bound(e, win) >= win.thr;
+        wide = __builtin_signbit(e.w);
       }
       if constexpr (CENSUS) {
-        const int n0 = has0 ? min(kGroup, nb - k0) : 0,
-                  n1 = has1 ? min(kGroup, nb - k0 - kGroup) : 0;
-        uint32_t tot = (uint32_t)(n0 + n1), ex = (uint32_t)((live0 ? n0 : 0) + (live1 ? n1 : 0));
+        const int n = has ? min(kGroup, nb - k0) : 0;
+        uint32_t tot = (uint32_t)n, ex = (uint32_t)(live ? n : 0);
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
           tot += __shfl_xor(tot, o, 64);
@@ -531,27 +542,50 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
         if (attempt == 0) cen.total += tot * (uint32_t)nvalid;
         cen.exec += ex * (uint32_t)nvalid;
         cen.shift += ex * (uint32_t)nvalid;
+        if (attempt > 0) cen.retry += ex * (uint32_t)nvalid;
+        if constexpr (F32) {
+          uint32_t wx = (uint32_t)(live && wide ? n : 0);
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) wx += __shfl_xor(wx, o, 64);
+          cen.wide += wx * (uint32_t)nvalid;
+        }
       }
       // (mode 3: the live wide blocks -- kF32Spread, flagged by the sign of
       // their envelope's a^2 -- go to a second, fp64 loop after the round)
-      uint64_t m0 = __ballot(live0 && !(F32 && wide0)), m1 = __ballot(live1 && !(F32 && wide1));
+      uint64_t mk = __ballot(live && !(F32 && wide));
       // software-pipelined as in lse_chunks
       int kg = 0;
-      bool have = next_live<STRIDE>(m0, m1, r0, kg);
+      bool have = next_live<STRIDE>(mk, r0, kg);
       if constexpr (F32) {
         const float Mf = (float)M;  // an integer (< 2^24 in magnitude): exact
         CoefGroup32 g32;
         if (have) load_group32(c32, kg, g32);
+        // two live blocks per iteration: their fp32 sums (terms <= 1, 16 of
+        // them) are added in fp32 and converted once (tools/fp32_pair_error.py
+        // blockf32_uu_pair: 2.3e-8 relative at config 4 against 2.2e-8)
         while (have) {
-          float d[KR][kGroup];
+          float d[KR][kGroup], b0[KR];
           lse_terms_f32<KR>(g32, Mf, y, d);
-          have = next_live<STRIDE>(m0, m1, r0, kg);
+          have = next_live<STRIDE>(mk, r0, kg);
           load_group32(c32, kg, g32);
           __builtin_amdgcn_sched_barrier(0);
-          lse_fold_shifted<KR>(d, s);
+          lse_block_sum<KR>(d, b0);
+          if (!have) {
+#pragma unroll
+            for (int r = 0; r < KR; ++r) s[r] += (double)b0[r];
+            break;
+          }
+          float b1[KR];
+          lse_terms_f32<KR>(g32, Mf, y, d);
+          have = next_live<STRIDE>(mk, r0, kg);
+          load_group32(c32, kg, g32);
+          __builtin_amdgcn_sched_barrier(0);
+          lse_block_sum<KR>(d, b1);
+#pragma unroll
+          for (int r = 0; r < KR; ++r) s[r] += (double)(b0[r] + b1[r]);
         }
-        uint64_t x0 = __ballot(live0 && wide0), x1 = __ballot(live1 && wide1);
-        while (next_live<STRIDE>(x0, x1, r0, kg)) {
+        uint64_t xk = __ballot(live && wide);
+        while (next_live<STRIDE>(xk, r0, kg)) {
           CoefGroup g;
           load_group(cs, kg, g);
           float d[KR][kGroup];
@@ -564,7 +598,7 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
         while (have) {
           float d[KR][kGroup];
           lse_terms_shifted<KR>(cgp, M, y, y2, d);
-          have = next_live<STRIDE>(m0, m1, r0, kg);
+          have = next_live<STRIDE>(mk, r0, kg);
           load_group(cs, kg, cgp);
           __builtin_amdgcn_sched_barrier(0);
           lse_fold_shifted<KR>(d, s);
@@ -884,7 +918,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
     // wave index as a scalar: the component addresses below are wave-uniform,
     // so the coefficients come in through scalar loads (SGPR operands)
     const int wv = __builtin_amdgcn_readfirstlane(wave);
-    LseCensus lcen{0u, 0u, 0u, 0u};
+    LseCensus lcen{0u, 0u, 0u, 0u, 0u, 0u};
     int nvalid = 0;
 #pragma unroll
     for (int r = 0; r < KR; ++r) nvalid += valid[r] ? 1 : 0;
@@ -925,14 +959,14 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
             // ~3 live blocks per pass.  Nothing compares the two tile shapes
             // bit for bit: batched, sharded and chunked runs of one draw take
             // the same tile shape.)
-            if (A.lse_prune > 2)  // block-local fp32 (Coef32) for the blocks that allow it
+            if (A.lse_prune > 2 || A.lse_f32)  // block-local fp32 (Coef32) where the block allows it
               lse_chunks<KR, CENSUS, 1, true>(
                   uniform_ptr(cm), cm, 0, K, y, lacc[mix], prune, win, nvalid, lcen,
                   uniform_ptr32(A.coef32 + (mix ? sa : sb) * (A.kcap / kCoefBlock)));
             else
               lse_chunks<KR, CENSUS, 1>(uniform_ptr(cm), cm, 0, K, y, lacc[mix], prune, win,
                                         nvalid, lcen);
-          } else if (A.lse_prune > 2) {
+          } else if (A.lse_prune > 2 || A.lse_f32) {
             lse_chunks<KR, CENSUS, kWaves, true>(
                 uniform_ptr(cm), cm, wv, K, y, lacc[mix], prune, win, nvalid, lcen,
                 uniform_ptr32(A.coef32 + (mix ? sa : sb) * (A.kcap / kCoefBlock)));
@@ -964,9 +998,10 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
     }
     if constexpr (CENSUS && LSE) {
       // nvalid is per lane: the per-lane sums add up to the wave's pairs
-      unsigned long long c2[4] = {lcen.total, lcen.exec, lcen.shift, lcen.f32};
+      unsigned long long c2[6] = {lcen.total, lcen.exec, lcen.shift, lcen.f32, lcen.retry,
+                                  lcen.wide};
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < 6; ++q) {
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) c2[q] += __shfl_xor(c2[q], o, 64);
       }
@@ -975,6 +1010,8 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
         atomicAdd(A.census + 4, c2[2]);
         atomicAdd(A.census + 5, c2[1]);
         atomicAdd(A.census + 6, c2[3]);
+        atomicAdd(A.census + 7, c2[4]);
+        atomicAdd(A.census + 8, c2[5]);
       }
     }
     if constexpr (!WT) {

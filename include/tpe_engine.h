@@ -276,9 +276,11 @@ int tpe_plan_set_lattice(tpe_plan_t p, int32_t enable);
  * zeros; a wave's retried pass counts again) -- and switch the census on (enable != 0)
  * or off for the following suggests.  counts has 6 entries.               */
 int tpe_plan_census(tpe_plan_t p, int32_t enable, int64_t *counts);
-/* The same with n_counts entries (up to 7): [6] of [5] the log-sum-exp pairs
+/* The same with n_counts entries (up to 9): [6] of [5] the log-sum-exp pairs
  * evaluated in the block-local fp32 per-group-lift form (prune mode 3 on
- * mixtures below the one-exponent size).                                   */
+ * mixtures below the one-exponent size), [7] of [4] the one-exponent pairs
+ * evaluated again by a wave's second attempt (its exponent re-centred),
+ * [8] of [4] the one-exponent pairs of wide blocks (mode 3's fp64 loop).   */
 int tpe_plan_census_n(tpe_plan_t p, int32_t enable, int64_t *counts, int32_t n_counts);
 
 /* Prior draws of n_suggest whole suggestions (rand.suggest, the TPE startup

@@ -64,7 +64,7 @@ def schemes(xc, w, mu, sg, low=-5.0, high=5.0):
     be32 = f32(2 * a2B * d)
     ga32 = f32(-a2B)
     order = np.argsort(xc, kind='stable')
-    out = {'current': np.empty(xc.size), 'blockf32': np.empty(xc.size)}
+    out = {k: np.empty(xc.size) for k in ('current', 'blockf32', 'blockf32_uu', 'blockf32_uu_pair')}
     for w0 in range(0, xc.size, 128):
         idx = order[w0:w0 + 128]
         y = xc[idx]
@@ -84,6 +84,19 @@ def schemes(xc, w, mu, sg, low=-5.0, high=5.0):
         e = np.exp2(zb.astype(np.float64)).astype(np.float32)
         s = e.sum(axis=2, dtype=np.float32).astype(np.float64).sum(axis=1)
         out['blockf32'][idx] = (M + np.log2(s)) / LOG2E
+        # round 4: gamma u^2 + (beta u + alpha'), u^2 rounded to fp32 once
+        u2 = np.broadcast_to(f32(u.astype(np.float64) ** 2)[:, :, None], uu.shape)
+        zc = fma32(np.broadcast_to(ga32, uu.shape), u2,
+                   fma32(np.broadcast_to(be32, uu.shape), uu, am))
+        e = np.exp2(zc.astype(np.float64)).astype(np.float32)
+        s = e.sum(axis=2, dtype=np.float32).astype(np.float64).sum(axis=1)
+        out['blockf32_uu'][idx] = (M + np.log2(s)) / LOG2E
+        # the same with two blocks' fp32 sums added in fp32 before the fp64 sum
+        bs = e.sum(axis=2, dtype=np.float32)                       # (n, nb) fp32
+        if nb % 2:
+            bs = np.concatenate([bs, np.zeros((bs.shape[0], 1), np.float32)], axis=1)
+        s2 = (bs[:, 0::2] + bs[:, 1::2]).astype(np.float64).sum(axis=1)
+        out['blockf32_uu_pair'][idx] = (M + np.log2(s2)) / LOG2E
     return out
 
 
