@@ -33,6 +33,8 @@ def short(name):
     base = m.group(1)
     if base == 'k_score' and ('ILb0ELb1E' in name or 'ILb1ELb1E' in name):
         return base + '_census'
+    if base == 'k_score_wave' and 'ILb1E' in name:   # k_score_wave<true>: census build
+        return base + '_census'
     return base
 
 
