@@ -391,18 +391,20 @@ __global__ __launch_bounds__(256) void k_micro(int iters, double *sink) {
     for (int c = 0; c < 4; ++c) acc += sm[c];
     if (acc == 12345.0) sink[t] = acc;
   } else if constexpr (WHICH == 6) {
-    // one log-sum-exp pair of prune mode 3 (lse_terms_f32): u = fp32(y' -
-    // centre) and u^2 once per (candidate, block), (A - M) + alpha per
-    // component, two packed fp32 FMAs per component pair (gamma u^2 + (beta u
-    // + alpha')), exp2, fp32 tree, fp64 sum; 4 candidates x 8 components
+    // one log-sum-exp pair of prune mode 3's one-exponent loop
+    // (lse_chunks_shifted): per (candidate, block of 8 components) u =
+    // fp32(y' - centre) and u^2, per block (A - M) + alpha, two packed fp32
+    // FMAs per component pair (gamma u^2 + (beta u + alpha')), exp2, the
+    // block's fp32 tree, two blocks' sums added in fp32, then one fp64 add;
+    // 4 candidates x 2 blocks of 8 components
     typedef float f2v __attribute__((ext_vector_type(2)));
     double y[4], sm[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) { y[c] = 1e-3 * (t + c); sm[c] = 0.0; }
-    float ca[8], cb[8], cc[8];
+    float ca[16], cb[16], cc[16];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) { ca[k] = -0.1f * k; cb[k] = 0.01f * k; cc[k] = -0.5f - 0.01f * k; }
-    const double centre = 0.25;
+    for (int k = 0; k < 16; ++k) { ca[k] = -0.1f * k; cb[k] = 0.01f * k; cc[k] = -0.5f - 0.01f * k; }
+    const double centre[2] = {0.25, 0.75};
     float A = 3.0f;
     const float Mf = 5.0f;
     for (int i = 0; i < iters; ++i) {
@@ -410,20 +412,26 @@ __global__ __launch_bounds__(256) void k_micro(int iters, double *sink) {
       const f2v am2 = {am, am};
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const float u = (float)(y[c] - centre);
-        const f2v u2 = {u, u};
-        const f2v uu2 = u2 * u2;
-        float e[8];
+        float bs[2];
 #pragma unroll
-        for (int k = 0; k < 8; k += 2) {
-          const f2v a2 = {ca[k], ca[k + 1]}, b2 = {cb[k], cb[k + 1]}, c2 = {cc[k], cc[k + 1]};
-          const f2v z = __builtin_elementwise_fma(c2, uu2, __builtin_elementwise_fma(b2, u2, a2 + am2));
-          e[k] = __builtin_amdgcn_exp2f(z.x);
-          e[k + 1] = __builtin_amdgcn_exp2f(z.y);
+        for (int b = 0; b < 2; ++b) {
+          const float u = (float)(y[c] - centre[b]);
+          const f2v u2 = {u, u};
+          const f2v uu2 = u2 * u2;
+          float e[8];
+#pragma unroll
+          for (int k = 0; k < 8; k += 2) {
+            const int q = 8 * b + k;
+            const f2v a2 = {ca[q], ca[q + 1]}, b2 = {cb[q], cb[q + 1]}, c2 = {cc[q], cc[q + 1]};
+            const f2v z = __builtin_elementwise_fma(c2, uu2, __builtin_elementwise_fma(b2, u2, a2 + am2));
+            e[k] = __builtin_amdgcn_exp2f(z.x);
+            e[k + 1] = __builtin_amdgcn_exp2f(z.y);
+          }
+          const float t0 = (e[0] + e[2]) + (e[1] + e[3]);
+          const float t1 = (e[4] + e[6]) + (e[5] + e[7]);
+          bs[b] = t0 + t1;
         }
-        const float t0 = (e[0] + e[2]) + (e[1] + e[3]);
-        const float t1 = (e[4] + e[6]) + (e[5] + e[7]);
-        sm[c] += (double)(t0 + t1);
+        sm[c] += (double)(bs[0] + bs[1]);
         y[c] += 1e-9;
       }
       A += 1e-7f;

@@ -623,44 +623,62 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
   return true;
 }
 
-// PRUNE setup: the wave's candidate range and, from the mixture's probe
-// component (its widest, the Parzen prior), a lower bound on every lane's
-// final exponent m (m >= max_k t_k >= t_probe).  Non-finite candidates or a
-// missing probe disable the skip (thr = -inf).
+// PRUNE setup, part 1 (once per wave, shared by both mixtures): the wave's
+// candidate range [lo, hi] (y' units, fp32 rounded outward) and whether
+// every valid candidate is finite.
+struct LseRange {
+  float lo, hi;
+  bool ok, any;
+};
 template <int KR>
-__device__ __forceinline__ LseWindow lse_window(KDbl *__restrict__ cs, int probe, int K,
-                                                const double (&y)[KR], const bool (&valid)[KR]) {
-  double lo = INFINITY, hi = -INFINITY, tmin = INFINITY;
-  bool ok = probe >= 0 && probe < K;
-  const int p = ok ? probe : 0;
-  const double px = cs[coef_off(p, 0)], py = cs[coef_off(p, 1)], pz = cs[coef_off(p, 2)];
+__device__ __forceinline__ LseRange lse_range(const double (&y)[KR], const bool (&valid)[KR]) {
+  double lo = INFINITY, hi = -INFINITY;
+  bool ok = true;
 #pragma unroll
   for (int r = 0; r < KR; ++r) {
     if (!valid[r]) continue;
     ok &= fabs(y[r]) < INFINITY;
     lo = fmin(lo, y[r]);
     hi = fmax(hi, y[r]);
-    tmin = fmin(tmin, fma(fma(pz, y[r], py), y[r], px));
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     lo = fmin(lo, __shfl_xor(lo, o, 64));
     hi = fmax(hi, __shfl_xor(hi, o, 64));
-    tmin = fmin(tmin, __shfl_xor(tmin, o, 64));
   }
-  ok = __all(ok) && tmin == tmin && tmin > -1.0e30;
-  // fp32 window rounded outward, threshold one unit conservative; the
-  // (wave-uniform) values travel in SGPRs
   const float flo = (float)lo, fhi = (float)hi;
-  float wl = ((double)flo > lo) ? nextafterf(flo, -INFINITY) : flo;
-  float wh = ((double)fhi < hi) ? nextafterf(fhi, INFINITY) : fhi;
-  const float dead = kLseDeadBase + (float)(32 - __builtin_clz((unsigned)max(K - 1, 1)));
-  float th = ok ? (float)(tmin - (double)dead) - 1.0f : -INFINITY;
-  if (!(lo <= hi)) th = -INFINITY;  // no valid candidate in the wave
+  const float wl = ((double)flo > lo) ? nextafterf(flo, -INFINITY) : flo;
+  const float wh = ((double)fhi < hi) ? nextafterf(fhi, INFINITY) : fhi;
   auto sf = [](float v) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
   };
-  return LseWindow{sf(wl), sf(wh), sf(th)};
+  return LseRange{sf(wl), sf(wh), __all(ok) != 0, lo <= hi};
+}
+
+// PRUNE setup, part 2 (per mixture): from the mixture's probe component (its
+// widest, the Parzen prior), a lower bound on every lane's final exponent m
+// (m >= max_k t_k >= t_probe) and with it the skip threshold.  Non-finite
+// candidates or a missing probe disable the skip (thr = -inf).
+template <int KR>
+__device__ __forceinline__ LseWindow lse_window(KDbl *__restrict__ cs, int probe, int K,
+                                                const double (&y)[KR], const bool (&valid)[KR],
+                                                const LseRange &rg) {
+  double tmin = INFINITY;
+  bool ok = rg.ok && probe >= 0 && probe < K;
+  const int p = ok ? probe : 0;
+  const double px = cs[coef_off(p, 0)], py = cs[coef_off(p, 1)], pz = cs[coef_off(p, 2)];
+#pragma unroll
+  for (int r = 0; r < KR; ++r)
+    if (valid[r]) tmin = fmin(tmin, fma(fma(pz, y[r], py), y[r], px));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) tmin = fmin(tmin, __shfl_xor(tmin, o, 64));
+  ok = ok && tmin == tmin && tmin > -1.0e30;
+  // threshold one unit conservative; the (wave-uniform) values travel in SGPRs
+  const float dead = kLseDeadBase + (float)(32 - __builtin_clz((unsigned)max(K - 1, 1)));
+  float th = ok ? (float)(tmin - (double)dead) - 1.0f : -INFINITY;
+  if (!rg.any) th = -INFINITY;  // no valid candidate in the wave
+  th = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, th)));
+  return LseWindow{rg.lo, rg.hi, th};
 }
 
 // CENSUS counts, per lane, the valid pairs, the live ones and the ones
@@ -816,6 +834,7 @@ struct ScoreSmem {
 #ifdef TPE_REREAD
   int64_t best_li[kWaves];
 #endif
+  uint32_t arrive;                      // wave tiles: waves done with the tile
 };
 
 #ifdef TPE_REREAD
@@ -846,6 +865,10 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
     if (tile == 0 && threadIdx.x == 0)
       A.results[(int64_t)s * A.n_hp + hp] = Partial{NAN, NAN, -1, 0, 0};
     return;
+  }
+  if constexpr (WT) {  // the block's arrival counter (finalize), before any wave can arrive
+    if (threadIdx.x == 0) sm.arrive = 0u;
+    __syncthreads();
   }
   const int64_t sb = 2 * (int64_t)hp, sa = sb + 1;
   const MixInfo ib = A.info[sb], ia = A.info[sa];
@@ -922,6 +945,10 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
     int nvalid = 0;
 #pragma unroll
     for (int r = 0; r < KR; ++r) nvalid += valid[r] ? 1 : 0;
+    LseRange rg{0.0f, 0.0f, false, false};
+    if constexpr (LSE) {
+      if (A.lse_prune != 0) rg = lse_range<KR>(y, valid);
+    }
 #pragma unroll
     for (int mix = 0; mix < 2; ++mix) {
       const Coef *__restrict__ cm = mix ? ca : cb;
@@ -929,7 +956,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
       if constexpr (LSE) {
         const bool prune = A.lse_prune != 0;
         LseWindow win{0.0f, 0.0f, -INFINITY};
-        if (prune) win = lse_window<KR>(uniform_ptr(cm), mix ? ia.probe : ib.probe, K, y, valid);
+        if (prune) win = lse_window<KR>(uniform_ptr(cm), mix ? ia.probe : ib.probe, K, y, valid, rg);
         // shifted single-exponent loop when the wave's window allows it
         // (lse_chunks_shifted's guard), else the exact per-group-lift loop
         // (mixtures of >= lse_shift_min components: fewer leave too few
@@ -1044,7 +1071,8 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
   SSTAMP(1);
   if (!WT && wave != 0) return;
 
-  // ---- finalize the tile (wave 0): lpdfs, EI, argmax (numpy semantics)
+  // ---- finalize (every wave of a wave tile, wave 0 of an 8-wave tile):
+  // lpdfs, EI, argmax (numpy semantics)
   double best_s = NAN, best_v = NAN;
   int64_t best_i = -1;
 #ifdef TPE_REREAD
@@ -1053,14 +1081,23 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
 #pragma unroll
   for (int r = 0; r < KR; ++r) {
     if (!valid[r]) continue;
-    double lpb, lpa;
+    double lpb = NAN, lpa = NAN, sc;
     if constexpr (LSE) {
       const double LN2 = 0.6931471805599453;
       const double2 b = WT ? sm.wpart[0][wave][r][lane] : sm.merged[0][r][lane];
       const double2 a = WT ? sm.wpart[1][wave][r][lane] : sm.merged[1][r][lane];
-      lpb = (b.x == -INFINITY) ? NAN : (b.x + log2(b.y)) * LN2;
-      lpa = (a.x == -INFINITY) ? NAN : (a.x + log2(a.y)) * LN2;
-      if constexpr (LOGN) { const double lx = log(x[r]); lpb -= lx; lpa -= lx; }
+      if (A.out_lb || A.out_la) {  // the lpdfs themselves (operator / parity paths)
+        lpb = (b.x == -INFINITY) ? NAN : (b.x + log2(b.y)) * LN2;
+        lpa = (a.x == -INFINITY) ? NAN : (a.x + log2(a.y)) * LN2;
+        if constexpr (LOGN) { const double lx = log(x[r]); lpb -= lx; lpa -= lx; }
+        sc = lpb - lpa;
+      } else {
+        // EI only (the suggest): ((m_b - m_a) + log2(s_b / s_a)) ln 2 -- one
+        // log2 instead of two, and LGMM's log x cancels; the exponents are
+        // integers (exact difference), a NaN / -inf lpdf gives a NaN score
+        sc = (b.x == -INFINITY || a.x == -INFINITY) ? NAN
+                                                    : ((b.x - a.x) + log2(b.y / a.y)) * LN2;
+      }
     } else if constexpr (ERF) {
       lpb = log(sm.merged[0][r][lane].x) - ib.log_pacc;
       lpa = log(sm.merged[1][r][lane].x) - ia.log_pacc;
@@ -1081,7 +1118,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
     const int64_t lo = cpos ? (int64_t)cpos[li[r]] : li[r];  // original position
     if (A.out_lb) A.out_lb[lo] = lpb;
     if (A.out_la) A.out_la[lo] = lpa;
-    const double sc = lpb - lpa;
+    if constexpr (!LSE) sc = lpb - lpa;
     const int64_t gi = A.cand_begin + lo;
     if (better(sc, gi, best_s, best_i)) {
       best_s = sc; best_v = x[r]; best_i = gi;
@@ -1091,10 +1128,8 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
     }
   }
 #ifdef TPE_REREAD
-  // the same reductions carrying the winner's bucketed slot, plus the two
-  // slots a re-read that does not carry it would take: lane 0's own best
-  // (not carried through the wave argmax) and wave 0's winner (not carried
-  // through the block argmax of the wave tiles)
+  // the same reduction carrying the winner's bucketed slot, plus the slot a
+  // re-read that does not carry it would take: lane 0's own best
   const int64_t dbg_own0 = __shfl(best_li, 0, 64);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -1102,17 +1137,36 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
     const int64_t oi = __shfl_xor(best_i, o, 64), ol = __shfl_xor(best_li, o, 64);
     if (better(os, oi, best_s, best_i)) { best_s = os; best_v = ov; best_i = oi; best_li = ol; }
   }
-  int64_t dbg_w0 = best_li;
+#else
+  wave_best(best_s, best_v, best_i);
+#endif
   if constexpr (WT) {
+    // the block's argmax over its wave tiles without a block barrier: each
+    // wave leaves its record in LDS and arrives on the block's LDS counter;
+    // the last to arrive merges the 8 records (better() orders ties by index,
+    // so arrival order does not matter) and publishes the tile -- the other
+    // waves exit at once instead of waiting for the block's slowest wave
     if (lane == 0) {
-      sm.best_s[wave] = best_s; sm.best_v[wave] = best_v; sm.best_i[wave] = best_i;
+      sm.best_s[wave] = best_s;
+      sm.best_v[wave] = best_v;
+      sm.best_i[wave] = best_i;
+#ifdef TPE_REREAD
       sm.best_li[wave] = best_li;
+#endif
     }
-    __syncthreads();
-    if (wave != 0) return;
-    dbg_w0 = best_li;
+    int last = 0;
+    if (lane == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      last = __hip_atomic_fetch_add(&sm.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ==
+             (uint32_t)kWaves - 1;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+    if (!__shfl(last, 0, 64)) return;
     const int w = lane < kWaves ? lane : 0;
-    best_s = sm.best_s[w]; best_v = sm.best_v[w]; best_i = lane < kWaves ? sm.best_i[w] : -1;
+    best_s = sm.best_s[w];
+    best_v = sm.best_v[w];
+    best_i = lane < kWaves ? sm.best_i[w] : -1;
+#ifdef TPE_REREAD
     best_li = sm.best_li[w];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -1120,21 +1174,14 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
       const int64_t oi = __shfl_xor(best_i, o, 64), ol = __shfl_xor(best_li, o, 64);
       if (better(os, oi, best_s, best_i)) { best_s = os; best_v = ov; best_i = oi; best_li = ol; }
     }
-  }
-  if (lane == 0 && s == 0 && (int64_t)hp * A.pstride + tile < (1 << 20)) {
-    g_tile_li[(int64_t)hp * A.pstride + tile][0] = dbg_w0;
-    g_tile_li[(int64_t)hp * A.pstride + tile][1] = dbg_own0;
-  }
 #else
-  wave_best(best_s, best_v, best_i);
-  if constexpr (WT) {  // the block's argmax over its wave tiles (better() orders ties)
-    if (lane == 0) { sm.best_s[wave] = best_s; sm.best_v[wave] = best_v; sm.best_i[wave] = best_i; }
-    __syncthreads();
-    if (wave != 0) return;
-    const int w = lane < kWaves ? lane : 0;
-    best_s = sm.best_s[w]; best_v = sm.best_v[w]; best_i = lane < kWaves ? sm.best_i[w] : -1;
     wave_best(best_s, best_v, best_i);
+#endif
   }
+  const int rix = tile, nrec = ntiles;
+#ifdef TPE_REREAD
+  if (lane == 0 && s == 0 && (int64_t)hp * A.pstride + rix < (1 << 20))
+    g_tile_li[(int64_t)hp * A.pstride + rix][1] = dbg_own0;
 #endif
   Partial *pbase = A.partial + ((int64_t)s * A.n_hp + hp) * A.pstride;
   int is_last = 0;
@@ -1144,7 +1191,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
     // with sc1 loads.  No L2 write-back / L1 invalidate fences (the
     // MI355X_MICROARCH.md "valid forms" row: one lane stores and signals, the
     // workgroup whose add returned last loads, all stores and loads sc1).
-    gu64 *rec = (gu64 *)(uintptr_t)(pbase + tile);
+    gu64 *rec = (gu64 *)(uintptr_t)(pbase + rix);
     __hip_atomic_store(rec + 0, dbits(best_s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(rec + 1, dbits(best_v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(rec + 2, (uint64_t)best_i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1154,7 +1201,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     gu32 *tk = (gu32 *)(uintptr_t)(A.ticket + (int64_t)s * A.n_hp + hp);
     const uint32_t t = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    is_last = (t == (uint32_t)ntiles - 1) ? 1 : 0;
+    is_last = (t == (uint32_t)nrec - 1) ? 1 : 0;
     if (is_last) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   is_last = __shfl(is_last, 0, 64);
@@ -1166,7 +1213,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
 #ifdef TPE_REREAD
   int64_t ft = -1;
 #endif
-  for (int i = lane; i < ntiles; i += 64) {
+  for (int i = lane; i < nrec; i += 64) {
     gu64 *rec = (gu64 *)(uintptr_t)(pbase + i);
     const double qs = bitsd(__hip_atomic_load(rec + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     const double qv = bitsd(__hip_atomic_load(rec + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -1194,7 +1241,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
         gu64 *rec = (gu64 *)(uintptr_t)(pbase + ft);
         const int64_t lt = (int64_t)__hip_atomic_load(rec + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const int64_t tix = (int64_t)hp * A.pstride + ft;
-        const int64_t lw0 = tix < (1 << 20) ? g_tile_li[tix][0] : -1;
+        const int64_t lw0 = -1;  // (no block argmax since round 4: per-wave records)
         const int64_t lown = tix < (1 << 20) ? g_tile_li[tix][1] : -1;
         const volatile double *vc = cand;
         const int64_t pos = fi - A.cand_begin;

@@ -9,8 +9,8 @@ finds at each candidate address a finalize could take:
                              wave and block argmax reductions
   pos    cand[index - begin] the global index taken as a slot (bucketed
                              arrays are not in index order)
-  w0     cand[li of wave 0]  the slot not carried through the block argmax of
-                             the wave tiles
+  (w0, the slot not carried through the block argmax of the wave tiles, was
+  a round-4 column: wave tiles publish per-wave records since, no block argmax)
   own0   cand[lane 0's li]   the slot not carried through the wave argmax
   row    cand[li ^ 64]       the same lane's other candidate row
 
@@ -56,7 +56,7 @@ def main():
         eng.lib.tpe_synchronize(eng.h)
         assert eng.lib.tpe_debug_reread(buf) == 0
         d = np.frombuffer(buf, dtype=np.float64).reshape(512, 20)
-        bad = {'reported': 0, 'slot': 0, 'pos': 0, 'w0': 0, 'own0': 0, 'row': 0, 'cpos': 0}
+        bad = {'reported': 0, 'slot': 0, 'pos': 0, 'own0': 0, 'row': 0, 'cpos': 0}
         near = []  # |other row - draw|: the row variant's values sit in the wave's window
         rows = []
         for h in dom.space.hps:
@@ -68,7 +68,6 @@ def main():
             bad['reported'] += fv != g
             bad['slot'] += v_slot != g
             bad['pos'] += v_pos != g
-            bad['w0'] += v_w0 != g
             bad['own0'] += v_own != g
             bad['row'] += d[i, 16] != g
             near.append(abs(d[i, 16] - g))
