@@ -8,7 +8,7 @@ of the whole job per second: for every active hyperparameter, candidates x
 (tpe.py:104-166, 259-301).  This is a reference-equivalent rate: pairs the
 engine skips are credited (their lpdf is produced) but not evaluated --
 log-sum-exp component blocks whose terms are bounded-negligible (each below
-2^-(31 + log2 K) of the candidate's largest term, <= 2^-30 relative on the
+2^-(27 + log2 K) of the candidate's largest term, <= 2^-26 relative on the
 lpdf), quantized terms that are exact zeros (both erf saturated), and
 candidates that read their lpdf off a value lattice.
 ``evaluated_pairs_per_s`` reports the pairs actually computed, side by side
@@ -576,7 +576,7 @@ def report(args, C, eng, world, mode, elapsed, value, pairs_step, pairs_suggest,
         'evaluated_fraction': (eval_step * world / pairs_step) if pairs_step else None,
         'evaluated_pairs_note': 'pairs actually computed per step, all ranks: log-sum-exp pairs '
                                 'outside the skipped component blocks (bounded-negligible: every '
-                                'skipped term < 2^-(31+log2 K) of the lane maximum, <= 2^-30 '
+                                'skipped term < 2^-(27+log2 K) of the lane maximum, <= 2^-26 '
                                 'relative on the lpdf), quantized pairs not skipped as exact '
                                 'zeros (both erf saturated), and value-lattice points x '
                                 'components; value credits every reference pair',

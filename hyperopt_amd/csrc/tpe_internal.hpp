@@ -85,8 +85,10 @@ struct MixInfo {
 // - D - 1 with D = kLseDeadBase + ceil(log2 K): each skipped term is below
 // 2^-(D+1) of the lane's largest term (>= 1/2 of the sum), so all skipped
 // terms of a K-component mixture move the lpdf by at most K * 2^-D <=
-// 2^-kLseDeadBase ~ 1e-9 relative -- 1000x inside the 1e-6 parity bar.
-constexpr float kLseDeadBase = 30.0f;
+// 2^-kLseDeadBase ~ 1.5e-8 relative -- 67x inside the 1e-6 parity bar.
+// (Round 4: 30 -> 26, a narrower live halo: config 4 277 -> 270 ms,
+// config 3 -1.6 %, config 5 -0.8 %, same box.)
+constexpr float kLseDeadBase = 26.0f;
 // census counters (tpe_plan_census_n): quantized total / live / evaluated,
 // log-sum-exp total / one-exponent evaluated / evaluated / evaluated in the
 // block-local fp32 per-group-lift form / one-exponent pairs of a wave's

@@ -19,9 +19,9 @@
 // Log-sum-exp (q = None): t = alpha + y'(beta + gamma y') (two fp64 FMAs, see
 // make_coef), 2^(t - m) with v_exp_f32 on the fp64 difference, fp32 group
 // sums added in fp64.  With value-bucketed candidates (large draws) a block
-// of 8 components whose envelope proves all its terms below 2^-(31 + log2 K)
+// of 8 components whose envelope proves all its terms below 2^-(27 + log2 K)
 // of every lane's largest term is skipped (lse_window, kLseDeadBase): the
-// lpdf moves by at most 2^-30 ~ 1e-9 relative.  Quantized: the reference's
+// lpdf moves by at most 2^-26 ~ 1.5e-8 relative.  Quantized: the reference's
 // sum_k w (Phi(ub) - Phi(lb)) in fp64 with OCML erf, in its operation order;
 // a component whose two erf arguments are beyond 6.5 on one side contributes
 // an exact 0 and is skipped when every candidate of the wave agrees.

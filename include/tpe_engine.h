@@ -294,8 +294,8 @@ int tpe_plan_sample_prior(tpe_plan_t p, const uint64_t *seeds, int64_t n_suggest
 
 /* Large draws score log-sum-exp candidates on value-bucketed tiles.  mode 1
  * skips the blocks of 8 mixture components whose every term is below
- * 2^-(31 + log2 K) of each candidate's largest one (lpdf moved by <= 2^-30
- * ~ 1e-9 relative); mode 2 also gives each wave one exponent instead of a
+ * 2^-(27 + log2 K) of each candidate's largest one (lpdf moved by <= 2^-26
+ * ~ 1.5e-8 relative); mode 2 also gives each wave one exponent instead of a
  * per-group max (terms 2^(t - M), M an upper bound of the wave's terms),
  * guarded so no term's fp32 argument exceeds ~|4| where it matters (<= 3e-7
  * relative; else the wave falls back to mode 1); mode 3 (default) computes

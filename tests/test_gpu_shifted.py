@@ -3,7 +3,7 @@
 At config 4 almost every evaluated (candidate, component) pair runs in the
 large-draw form: candidates value-bucketed in 4096-candidate blocks
 (k_draw_sorted), log-sum-exp component blocks whose terms are provably below
-2^-(31 + log2 K) of the lane maximum skipped, and one exponent per wave
+2^-(27 + log2 K) of the lane maximum skipped, and one exponent per wave
 (``lse_chunks_shifted``: prune mode 2 with an fp64 quadratic, mode 3 -- the
 default -- with the block-local fp32 quadratic).  These tests anchor that form to the
 CPU oracle (the float64 restatement of tpe.py:104-166 / 259-301 with

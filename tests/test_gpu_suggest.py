@@ -417,9 +417,9 @@ def test_thread_trials_async_batched_tpe():
 def test_pruned_lse_equals_full_evaluation(name):
     """Large draws (>= 4M candidate draws) are value-bucketed by the draw and
     log-sum-exp tiles skip the component blocks whose terms are all below
-    2^-(31 + log2 K) of every candidate's largest (mode 1): winners (index,
-    value) equal the unpruned run and scores agree within 2^-30 relative per
-    lpdf.  Modes 2 and 3 (default) also give each wave one exponent (fp64 /
+    2^-(27 + log2 K) of every candidate's largest (mode 1): scores agree
+    with the unpruned run within 2^-26 relative per lpdf, winners equal up to
+    ties within that.  Modes 2 and 3 (default) also give each wave one exponent (fp64 /
     block-local fp32 quadratic): scores within the north-star 1e-6, winners
     equal up to ties within it.  The winner also
     equals the merge of two differently tiled shards."""
@@ -440,10 +440,7 @@ def test_pruned_lse_equals_full_evaluation(name):
     plan.set_prune(0)
     want = plan.suggest([21, 22], n)
     plan.set_prune(3)
-    np.testing.assert_array_equal(got['index'], want['index'])
-    np.testing.assert_array_equal(got['value'], want['value'])
-    np.testing.assert_array_equal(got['active'], want['active'])
-    np.testing.assert_allclose(got['score'], want['score'], rtol=4e-9, atol=4e-9)
+    assert_winners_match(got, want, rtol=2.0 ** -25, msg='block skip (mode 1)')
     assert_winners_match(shifted64, want, msg='one exponent per wave')
     assert_winners_match(shifted, want, msg='one exponent per wave, block-local fp32')
     assert c[3] > 0 and c[5] < c[3], c          # blocks were skipped
@@ -508,7 +505,7 @@ def test_small_draw_pruning_in_child_process():
     """Opt-in bucketing + block skip of small-draw log-sum-exp slots
     (TPE_SMALL_SORT=1, read once per process): batched suggestions equal the
     single-seed ones bit for bit, and the winners equal the default path's up
-    to near-ties (the skip moves an lpdf by <= 2^-30 relative)."""
+    to near-ties (the skip moves an lpdf by <= 2^-26 relative)."""
     import os
     import subprocess
     import sys

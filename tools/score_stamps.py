@@ -33,11 +33,16 @@ def main(cfg, n_cand):
     hps, conds, pprior = dom.space.engine_tables()
     plan = E.Plan(eng, hps, conds, pprior, max_trials=losses.size)
     plan.set_history(losses, vals, active)
+    lv = int(os.environ.get('TPE_STAMPS_LEVEL', '-1'))
     for i in range(5):
         plan.fit(gamma=0.25, prior_weight=1.0, lf=25)
-        # TPE_STAMPS_LEVEL=l: stop after level l (its launch is the last one)
-        plan.suggest([7 + i], n_cand, level=int(os.environ.get('TPE_STAMPS_LEVEL', '-1')),
-                     fetch=False)
+        # TPE_STAMPS_LEVEL=l: levels 0 .. l, one call each (level l's launch
+        # is the last one: its stamps are the ones read)
+        if lv < 0:
+            plan.suggest([7 + i], n_cand, fetch=False)
+        else:
+            for l in range(lv + 1):
+                plan.suggest([7 + i], n_cand, level=l, fetch=False)
     eng.lib.tpe_synchronize(eng.h)
     buf = (C.c_ulonglong * (8192 * 4))()
     assert eng.lib.tpe_debug_score_stamps(buf) == 0
