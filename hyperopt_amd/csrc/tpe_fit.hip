@@ -50,7 +50,7 @@ constexpr int kSortCap = 10000;              // elements sorted in LDS (u16 posi
 constexpr int kMixLds = 4097;                // K kept in LDS until copy-out (m <= 4096)
 constexpr int kMixStride = 4104;             // doubles per LDS mixture array
 constexpr int kDigits = 256;
-constexpr int kPreN = 4 * kFitThreads;       // histories held in registers by k_fit
+constexpr int kPreN = 12 * kFitThreads;      // histories whose values k_fit prefetches
 
 // dynamic LDS map (bytes)
 constexpr int kOffKeys = 0;                               // u64 [kSortCap]
@@ -85,13 +85,16 @@ __device__ __forceinline__ NpNode np_node(int len, int id) {
   return NpNode{lo, n};
 }
 
+constexpr int kGatherRows = 12;  // trials per thread in one gather chunk (12288 per block)
 struct GatherEx {  // one wave's share of a gather chunk
-  int cnt, nlt;
+  int nlt, pad;
   uint64_t kand, kor;
 };
 
 struct FitShared {
-  GatherEx gx[2][kFitWaves];
+  GatherEx gx[1][kFitWaves];
+  int gcnt[kGatherRows][kFitWaves];  // selected trials per (row, wave) of a gather chunk
+  int gbase[kGatherRows][kFitWaves]; // their exclusive prefix in (row, wave) order
   double val[2][kNpHeap];    // pairwise-sum node values by heap id (two arrays at once)
   uint64_t rk[2][kFitWaves];
   uint32_t rp[2][kFitWaves];
@@ -340,7 +343,9 @@ __device__ __forceinline__ bool merge_sort_packed(const uint64_t *keys, int n, i
     kb0[e] = k[u];
     pb0[e] = (uint16_t)p[u];
   }
+  STAMP(21);
   __syncthreads();
+  STAMP(22);
   // 4-way merge levels (64 -> 256 -> 1024 [-> 4096]): an element's position in
   // its quad of runs is its index in its own run plus its rank in each of the
   // three others, three branch-free binary searches side by side -- half the
@@ -388,6 +393,7 @@ __device__ __forceinline__ bool merge_sort_packed(const uint64_t *keys, int n, i
       k[u] = sk[u * kFitThreads + t];
       p[u] = sp[u * kFitThreads + t];
     }
+    STAMP(23 + (__builtin_ctz((unsigned)len) - 6) / 2);
   }
   // runs of equal truncated keys (sorted by position so far) are ranked by
   // their full keys; a run longer than kRunMax sends the block to the full sort
@@ -422,7 +428,10 @@ __device__ __forceinline__ bool merge_sort_packed(const uint64_t *keys, int n, i
       }
     }
   }
-  return !__syncthreads_or(bad);
+  STAMP(26);
+  const bool ok = !__syncthreads_or(bad);
+  STAMP(27);
+  return ok;
 }
 
 template <typename PosT, bool SMALL = false>
@@ -648,46 +657,55 @@ struct TiedPosAt {  // positions of the trials whose key equals T
   __device__ uint64_t operator()(int j) const { return keys[j] == T ? (uint64_t)j : ~0ull; }
 };
 
-// One radix-select step: histogram (wave-aggregated LDS atomics) of the
-// 8-bit digit at `shift` of the values v(j) whose bits under `mask` equal
-// `prefix`, then the digit holding the need-th (1-based) smallest; `need`
-// becomes the rank inside that digit.
+// One radix-select step: histogram of the 8-bit digit at `shift` of the
+// values v(j) whose bits under `mask` equal `prefix` -- each wave counts into
+// its own 256 bins (cnt[wave][256]) with one LDS atomic per value (an 8-ballot
+// match per 64 values to elect one adder per distinct digit cost ~20
+// instructions per value: 3-8 us of a 1e4-trial split), the bins summed per
+// digit into tot[256] -- then the digit holding the need-th (1-based)
+// smallest; `need` becomes the rank inside it.
 template <typename ValFn>
 __device__ __forceinline__ Digit select_digit(ValFn val, int n, uint64_t mask, uint64_t prefix, int shift,
-                                       uint32_t need, uint32_t *hist, FitShared &sm, int par) {
+                                       uint32_t need, uint32_t *cnt, uint32_t *tot, FitShared &sm,
+                                       int par) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  // hist[0..256) is zero on entry; zero the other half for the next step
-  // (nobody reads it before this step's first barrier)
-  uint32_t *other = par ? hist - kDigits : hist + kDigits;
-  for (int d = threadIdx.x; d < kDigits; d += blockDim.x) other[d] = 0;
+  uint32_t *mine = cnt + w * kDigits;
+  for (int d = lane; d < kDigits; d += 64) mine[d] = 0;
   STAMP(16);
+  // (a wave's LDS operations complete in order: its zeroing precedes its adds)
   for (int j0 = 0; j0 < n; j0 += blockDim.x) {
     const int j = j0 + threadIdx.x;
     const uint64_t x = j < n ? val(j) : 0ull;
     const bool v = j < n && (x & mask) == prefix;
-    const uint32_t d = v ? (uint32_t)(x >> shift) & 255u : 0u;
-    const uint64_t mt = match8(d, v);
-    if (v && lane == __ffsll((long long)mt) - 1) atomicAdd(&hist[d], (uint32_t)__popcll(mt));
+    if (v) __hip_atomic_fetch_add(&mine[(uint32_t)(x >> shift) & 255u], 1u, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   STAMP(17);
   __syncthreads();
   STAMP(18);
+  if (threadIdx.x < kDigits) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int q = 0; q < kFitWaves; ++q) c += cnt[q * kDigits + threadIdx.x];
+    tot[threadIdx.x] = c;
+  }
+  __syncthreads();
   if (w == 0) {
-    const uint4 c = *reinterpret_cast<const uint4 *>(hist + 4 * lane);
+    const uint4 c = *reinterpret_cast<const uint4 *>(tot + 4 * lane);
     const uint32_t ls = c.x + c.y + c.z + c.w;
     const uint32_t before = wave_excl_scan_u32(ls);
     if (before < need && need <= before + ls) {  // the digit reaching `need`
-      uint32_t acc = before, dd = 4 * lane, cnt = c.x;
+      uint32_t acc = before, dd = 4 * lane, cn = c.x;
       if (acc + c.x < need) {
-        acc += c.x; dd += 1; cnt = c.y;
+        acc += c.x; dd += 1; cn = c.y;
         if (acc + c.y < need) {
-          acc += c.y; dd += 1; cnt = c.z;
-          if (acc + c.z < need) { acc += c.z; dd += 1; cnt = c.w; }
+          acc += c.y; dd += 1; cn = c.z;
+          if (acc + c.z < need) { acc += c.z; dd += 1; cn = c.w; }
         }
       }
       sm.rp[par][0] = dd;
       sm.rp[par][1] = need - acc;
-      sm.rp[par][2] = cnt;
+      sm.rp[par][2] = cn;
     }
   }
   STAMP(19);
@@ -699,40 +717,37 @@ __device__ __forceinline__ Digit select_digit(ValFn val, int n, uint64_t mask, u
 // (a2) the n_below-th smallest (loss key, position) by radix select over the
 // 64-bit keys (digits constant over all losses skipped), then -- only when
 // several trials tie on that loss -- over the positions of the tied ones.
-// pre: the block holds the history in registers (n <= kPreN, trials
-// 4 t .. 4 t + 3 of thread t, see Prefetch); otherwise losses are read here.
+// The losses are read here (four loads in flight per thread); their keys
+// stay in LDS (up to kSortCap trials, else the global copy) for the gather.
 template <bool SMALL = false>
-__device__ __forceinline__ Split compute_split(const FitArgs &A, const FitCtx &C, FitShared &sm,
-                                               bool pre, const double (&pls)[4]) {
+__device__ __forceinline__ Split compute_split(const FitArgs &A, const FitCtx &C, FitShared &sm) {
   const int n = (int)A.n;
   const int nb = A.n_below;
   if (nb <= 0 || n == 0) return Split{0, 0, 0};
   if (nb >= n) return Split{0, 0, 1};
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   uint64_t *lk = reinterpret_cast<uint64_t *>(C.lds + kOffKeys);
-  uint32_t *hist = reinterpret_cast<uint32_t *>(C.lds + kOffCnt);
+  uint32_t *cnt = reinterpret_cast<uint32_t *>(C.lds + kOffCnt);  // [16 waves][256]
+  uint32_t *tot = reinterpret_cast<uint32_t *>(C.lds + kOffRun);  // [256]
   uint64_t *keys = (SMALL || n <= kSortCap) ? lk : C.gkeys;
-  for (int d = threadIdx.x; d < kDigits; d += blockDim.x) hist[d] = 0;
   STAMP(31);
   uint64_t an = ~0ull, on = 0ull;
-  if (pre) {
-    constexpr int PER = SMALL ? 1 : 4;  // trials per thread in registers
+  {
+    // four loads in flight per thread before their keys are stored
+    for (int j0 = threadIdx.x; j0 < n; j0 += 4 * (int)blockDim.x) {
+      double l[4];
 #pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int j = PER * threadIdx.x + u;
-      if (j < n) {
-        const uint64_t k = sort_key(pls[u]);
-        lk[j] = k;
-        an &= k;
-        on |= k;
+      for (int u = 0; u < 4; ++u) l[u] = A.losses[min(j0 + u * (int)blockDim.x, n - 1)];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int j = j0 + u * (int)blockDim.x;
+        if (j < n) {
+          const uint64_t k = sort_key(l[u]);
+          keys[j] = k;
+          an &= k;
+          on |= k;
+        }
       }
-    }
-  } else {
-    for (int j = threadIdx.x; j < n; j += blockDim.x) {
-      const uint64_t k = sort_key(A.losses[j]);
-      keys[j] = k;
-      an &= k;
-      on |= k;
     }
   }
   STAMP(32);
@@ -755,8 +770,7 @@ __device__ __forceinline__ Split compute_split(const FitArgs &A, const FitCtx &C
   for (int shift = 56; shift >= 0; shift -= 8) {
     const uint64_t dm = 255ull << shift;
     if ((vary & dm) == 0) continue;
-    const Digit g = select_digit(kv, n, mask, prefix, shift, need, hist + kDigits * (step & 1),
-                                 sm, step & 1);
+    const Digit g = select_digit(kv, n, mask, prefix, shift, need, cnt, tot, sm, step & 1);
     ++step;
     need = g.need;
     prefix |= (uint64_t)g.d << shift;
@@ -774,7 +788,7 @@ __device__ __forceinline__ Split compute_split(const FitArgs &A, const FitCtx &C
   const TiedPosAt pv{keys, T};
   for (int shift = 24; shift >= 0; shift -= 8) {
     const Digit g = select_digit(pv, n, pmask | 0xFFFFFFFF00000000ull, pprefix, shift, need,
-                                 hist + kDigits * (step & 1), sm, step & 1);
+                                 cnt, tot, sm, step & 1);
     ++step;
     need = g.need;
     pprefix |= (uint64_t)g.d << shift;
@@ -1144,29 +1158,37 @@ __device__ __forceinline__ void fit_slot(const FitArgs &A, unsigned char *dyn_ld
 #ifdef TPE_STAMPS
   const unsigned long long clk0 = clock64();  // shader clock: SCLK = cycles / wall time
 #endif
-  // small histories: every trial's (loss, value, activity) is loaded into
-  // registers up front, so the gather below needs no second memory round trip
+  // histories of <= kPreN trials: every trial's value and activity is loaded
+  // into registers up front (in flight during the split), so the gather
+  // below needs no memory round trip; the losses' sort keys come from the
+  // split's copy
   const bool pre = SMALL || A.n <= kPreN;
-  constexpr int PER = SMALL ? 1 : 4;  // consecutive trials per thread (gather, prefetch)
+  constexpr int PER = SMALL ? 1 : kGatherRows;  // rows: trial c0 + u * 1024 + t
   const double *row = A.vals + (int64_t)hp * A.ld;
   const uint8_t *arow = A.active + (int64_t)hp * A.ld;
-  double pls[4] = {0.0, 0.0, 0.0, 0.0}, prv[4] = {0.0, 0.0, 0.0, 0.0};
-  uint8_t pac[4] = {0, 0, 0, 0};
+  double prv[PER];
+  uint8_t pac[PER];
   if (pre) {
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
-      const int64_t j = min<int64_t>(PER * (int64_t)threadIdx.x + u, A.n - 1);
+      const int64_t j = min<int64_t>((int64_t)u * kFitThreads + threadIdx.x, A.n - 1);
       pac[u] = j >= 0 ? arow[j] : 0;
-      pls[u] = j >= 0 ? A.losses[j] : 0.0;
       prv[u] = j >= 0 ? row[j] : 0.0;
     }
   }
-  const Split t = compute_split<SMALL>(A, C, sm, pre, pls);
+  const Split t = compute_split<SMALL>(A, C, sm);
   __syncthreads();
   STAMP(1);
 
   // ---- gather this side's observations in tid order (tpe.py:629-636):
-  // 4 consecutive trials per thread, one block scan per 4096 trials
+  // chunks of PER * 1024 trials, trial c0 + u * 1024 + t in thread t's row u
+  // (coalesced loads); the order inside a chunk is u-major, so a selected
+  // trial's slot is the chunk base + the trials selected in earlier (row,
+  // wave) pairs + its rank in its wave's ballot of row u.  The chunks move
+  // raw values only; the transform (a float64 log for the log families) and
+  // the sort keys run afterwards over the m gathered values, densely (a
+  // conditional hp's side is a sparse subset of the rows: transformed in
+  // place, every row with one selected lane would cost the whole wave a log)
   const bool cat = H.family == TPE_CAT;
   // observations: LDS above the keys when the history is small (no global
   // stores in flight at the barriers that follow), else slot scratch
@@ -1174,79 +1196,90 @@ __device__ __forceinline__ void fit_slot(const FitArgs &A, unsigned char *dyn_ld
                    ? reinterpret_cast<double *>(dyn_lds + kOffKeys + 8 * kMergeMax)
                    : A.ob + slot * A.kcap;
   uint64_t *lk = reinterpret_cast<uint64_t *>(dyn_lds + kOffKeys);
-  int m = 0, nlt = 0;
-  uint64_t kand = ~0ull, kor = 0ull;  // bits equal over all keys: kand == kor there
-  const double ofloor = obs_floor(H.obs_transform, H.low);
+  // the split's loss keys (compute_split: LDS up to kSortCap trials)
+  const uint64_t *lkey = (SMALL || A.n <= kSortCap) ? lk : C.gkeys;
+  int m = 0;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  int chunk = 0;
-  for (int64_t c0 = 0; c0 < A.n; c0 += PER * kFitThreads, ++chunk) {
-    const int64_t j0 = c0 + PER * (int64_t)threadIdx.x;
-    bool f[4];
-    double v[4];
-    int cntl = 0;
-    // all loads issued before any use: one memory round trip per chunk
-    uint8_t ac[4];
-    double ls[4], rv[4];
-    if (pre) {
-#pragma unroll
-      for (int u = 0; u < PER; ++u) { ac[u] = pac[u]; ls[u] = pls[u]; rv[u] = prv[u]; }
-    } else {
+  for (int64_t c0 = 0; c0 < A.n; c0 += PER * kFitThreads) {
+    if (!pre) {  // all loads issued before any use: one memory round trip per chunk
 #pragma unroll
       for (int u = 0; u < PER; ++u) {
-        const int64_t j = min<int64_t>(j0 + u, A.n - 1);
-        ac[u] = arow[j];
-        ls[u] = A.losses[j];
-        rv[u] = row[j];
+        const int64_t j = min<int64_t>(c0 + (int64_t)u * kFitThreads + threadIdx.x, A.n - 1);
+        pac[u] = arow[j];
+        prv[u] = row[j];
       }
     }
+    uint32_t fm = 0u;
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
-      const int64_t j = j0 + u;
-      f[u] = j < A.n && ac[u] && (is_below(t, sort_key(ls[u]), (uint32_t)j) == (side == 0));
-      v[u] = 0.0;
-      if (f[u]) {
-        v[u] = obs_transform(rv[u], H.obs_transform, ofloor);
-        nlt += (v[u] < H.prior_mu) ? 1 : 0;
-        const uint64_t k = cat ? (uint64_t)(int64_t)v[u] : sort_key(v[u]);
-        kand &= k;
-        kor |= k;
-      }
-      cntl += f[u] ? 1 : 0;
+      const int64_t j = c0 + (int64_t)u * kFitThreads + threadIdx.x;
+      const bool f = j < A.n && pac[u] && (is_below(t, lkey[j], (uint32_t)j) == (side == 0));
+      fm |= f ? 1u << u : 0u;
+      const uint64_t b = __ballot(f);
+      if (lane == 0) sm.gcnt[u][wv] = (int)__popcll(b);
     }
     STAMP(35);
-    // one exchange per chunk (double-buffered by chunk parity, so a single
-    // barrier): the wave's count for the scan, and the running nlt / key-bit
-    // reductions, which are final after the last chunk
-    const int x = wave_incl_scan(cntl);
-    const int nw = wave_sum(nlt);
-    const uint64_t aw = wave_and(kand), ow = wave_or(kor);
-    GatherEx &ex = sm.gx[chunk & 1][wv];
-    if (lane == 63) { ex.cnt = x; ex.nlt = nw; ex.kand = aw; ex.kor = ow; }
     __syncthreads();
-    int before = 0, tot = 0, nl = 0;
-    uint64_t ka = ~0ull, ko = 0ull;
+    // (row, wave) exclusive prefix of the counts, by wave 0: lane l takes the
+    // consecutive entries [l * E, l * E + E) of the row-major table
+    if (wv == 0) {
+      constexpr int NE = PER * kFitWaves, E = (NE + 63) / 64;
+      const int *gc = &sm.gcnt[0][0];
+      int *gb = &sm.gbase[0][0];
+      int c[E], loc = 0;
 #pragma unroll
-    for (int i = 0; i < kFitWaves; ++i) {
-      const GatherEx &e = sm.gx[chunk & 1][i];
-      before += (i < wv) ? e.cnt : 0;
-      tot += e.cnt;
-      nl += e.nlt;
-      ka &= e.kand;
-      ko |= e.kor;
+      for (int e = 0; e < E; ++e) {
+        const int q = lane * E + e;
+        c[e] = q < NE ? gc[q] : 0;
+        loc += c[e];
+      }
+      int acc = wave_incl_scan(loc) - loc;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int q = lane * E + e;
+        if (q < NE) gb[q] = acc;
+        acc += c[e];
+      }
     }
+    __syncthreads();
     STAMP(36);
-    int i = m + before + x - cntl;
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
-      if (!f[u]) continue;
-      ob[i] = v[u];
-      const uint64_t k = cat ? (uint64_t)(int64_t)v[u] : sort_key(v[u]);  // (recomputed: registers)
-      if (i < kSortCap) lk[i] = k;
-      else C.gkeys[i] = k;
-      ++i;
+      const bool f = (fm >> u) & 1u;
+      const uint64_t b = __ballot(f);
+      if (f) ob[m + sm.gbase[u][wv] + (int)__popcll(b & lanemask_lt())] = prv[u];
     }
-    m += tot;
-    if (c0 + PER * kFitThreads >= A.n) { nlt = nl; kand = ka; kor = ko; }  // block totals
+    m += sm.gbase[PER - 1][kFitWaves - 1] + sm.gcnt[PER - 1][kFitWaves - 1];
+    __syncthreads();  // (the next chunk's counts reuse gcnt / gbase; ob complete)
+  }
+  // transform in place, sort keys, and the block's count below the prior mean
+  // and key-bit reductions (bits equal over all keys: kand == kor there)
+  const double ofloor = obs_floor(H.obs_transform, H.low);
+  int nlt = 0;
+  uint64_t kand = ~0ull, kor = 0ull;
+  for (int i = threadIdx.x; i < m; i += kFitThreads) {
+    const double v = obs_transform(ob[i], H.obs_transform, ofloor);
+    ob[i] = v;
+    nlt += (v < H.prior_mu) ? 1 : 0;
+    const uint64_t k = cat ? (uint64_t)(int64_t)v : sort_key(v);
+    kand &= k;
+    kor |= k;
+    if (i < kSortCap) lk[i] = k;
+    else C.gkeys[i] = k;
+  }
+  {
+    const int nw = wave_sum(nlt);
+    const uint64_t aw = wave_and(kand), ow = wave_or(kor);
+    if (lane == 0) { sm.gx[0][wv].nlt = nw; sm.gx[0][wv].kand = aw; sm.gx[0][wv].kor = ow; }
+    __syncthreads();
+    nlt = 0;
+#pragma unroll
+    for (int i = 0; i < kFitWaves; ++i) {
+      const GatherEx &e = sm.gx[0][i];
+      nlt += e.nlt;
+      kand &= e.kand;
+      kor |= e.kor;
+    }
   }
   STAMP(37);
   const uint64_t vary = kand ^ kor;
@@ -1304,8 +1337,7 @@ __global__ __launch_bounds__(kFitThreads) void k_split(FitArgs A, uint8_t *__res
   C.gkeys = reinterpret_cast<uint64_t *>(A.sortbuf);
   C.gpa = reinterpret_cast<uint32_t *>(A.sortbuf + 8 * A.scap);
   C.gpb = C.gpa + A.scap;
-  const double none[4] = {0.0, 0.0, 0.0, 0.0};
-  const Split t = compute_split(A, C, sm, false, none);
+  const Split t = compute_split(A, C, sm);
   for (int64_t j = threadIdx.x; j < A.n; j += blockDim.x)
     below[j] = is_below(t, sort_key(A.losses[j]), (uint32_t)j) ? 1 : 0;
 }

@@ -49,8 +49,8 @@ def main(cfg, slots):
                                                    (row[0] - t0) / 100.0) + ' '.join(marks))
     print('kernel span: %.1f us' % ((st[:2 * P, 10].max() - t0) / 100.0))
     sub = {16: 'sd.zero', 17: 'sd.hist', 18: 'sd.bar1', 19: 'sd.scan', 20: 'sd.bar2',
-           21: 'ms.load', 22: 'ms.bitonic64', 23: 'ms.bar', 24: 'ms.L64', 25: 'ms.L128',
-           26: 'ms.L256', 27: 'ms.L512', 28: 'np.plan', 29: 'np.leaves', 30: 'np.end',
+           21: 'ms.load', 22: 'ms.bitonic64', 23: 'ms.bar|L64', 24: 'ms.L64|256', 25: 'ms.L128|1024',
+           26: 'ms.L256|fix', 27: 'ms.L512|or', 28: 'np.plan', 29: 'np.leaves', 30: 'np.end',
            31: 'k.zero', 32: 'k.load', 33: 'k.wred', 34: 'k.bar', 35: 'g.load', 36: 'g.scan', 37: 'g.write',
            38: 'rs.init', 39: 'rs.pass', 40: 'cat.seg', 41: 'cat.lfw'}
     slowest = int(np.argmax(st[:2 * P, 10] - st[:2 * P, 0]))
