@@ -54,7 +54,8 @@ def main(cfg, slots):
            31: 'k.zero', 32: 'k.load', 33: 'k.wred', 34: 'k.bar', 35: 'g.load', 36: 'g.scan', 37: 'g.write',
            38: 'rs.init', 39: 'rs.pass', 40: 'cat.seg', 41: 'cat.lfw'}
     slowest = int(np.argmax(st[:2 * P, 10] - st[:2 * P, 0]))
-    for slot in sorted(set(range(min(2 * P, 4))) | {slowest}):
+    extra = {int(v) for v in os.environ.get('TPE_STAMPS_DETAIL', '').split(',') if v}
+    for slot in sorted(set(range(min(2 * P, 4))) | {slowest} | {e for e in extra if e < 2 * P}):
         row = st[slot]
         print('slot %d last sub-phase stamps (us from slot start): ' % slot + ' '.join(
             '%s=%.2f' % (nm, (row[i] - row[0]) / 100.0) for i, nm in sub.items() if row[i] >= row[0]))
