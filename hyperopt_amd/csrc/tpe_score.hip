@@ -845,6 +845,16 @@ __device__ double g_reread[512][20];
 __device__ int64_t g_tile_li[1 << 20][2];
 #endif
 
+#ifdef TPE_REREAD2
+// diagnostic build only (make dbg4; tools/reread_shard.py): at finalize,
+// every valid wave-tile row compares the candidate it scored (registers) with
+// a plain and a volatile re-read of the same slot; [0] rows, [1] plain
+// differs, [2] volatile differs, [3] examples taken; then up to 64 examples
+// of (li, cpos[li], x, plain, volatile, chunk begin, n_cand, hp)
+__device__ unsigned long long g_rr2_cnt[4];
+__device__ double g_rr2_ex[64][8];
+#endif
+
 template <int KIND, bool CENSUS>
 __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, int slot, int tile,
                                            int ntiles, bool known_active) {
@@ -1082,6 +1092,35 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
   for (int r = 0; r < KR; ++r) {
     if (!valid[r]) continue;
     double lpb = NAN, lpa = NAN, sc;
+#ifdef TPE_REREAD3
+    // (diagnostic build dbg5: the winner's value taken from a plain re-read)
+    if constexpr (LSE && WT) x[r] = cand[li[r]];
+#endif
+#ifdef TPE_REREAD2
+    if constexpr (LSE && WT) {
+      const double xp = cand[li[r]];
+      const double xv = *(const volatile double *)&cand[li[r]];
+      const bool dp = xp != x[r] && !(xp != xp && x[r] != x[r]);
+      const bool dv = xv != x[r] && !(xv != xv && x[r] != x[r]);
+      atomicAdd(&g_rr2_cnt[0], 1ull);
+      if (dp) atomicAdd(&g_rr2_cnt[1], 1ull);
+      if (dv) atomicAdd(&g_rr2_cnt[2], 1ull);
+      if (dp || dv) {
+        const unsigned long long e = atomicAdd(&g_rr2_cnt[3], 1ull);
+        if (e < 64) {
+          double *o = g_rr2_ex[e];
+          o[0] = (double)li[r];
+          o[1] = cpos ? (double)cpos[li[r]] : -1.0;
+          o[2] = x[r];
+          o[3] = xp;
+          o[4] = xv;
+          o[5] = (double)A.cand_begin;
+          o[6] = (double)A.n_cand;
+          o[7] = (double)hp;
+        }
+      }
+    }
+#endif
     if constexpr (LSE) {
       const double LN2 = 0.6931471805599453;
       const double2 b = WT ? sm.wpart[0][wave][r][lane] : sm.merged[0][r][lane];
@@ -1282,6 +1321,19 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
 extern "C" int tpe_debug_reread(double *out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(tpe::g_reread), sizeof(tpe::g_reread)) == hipSuccess
              ? 0 : -5;
+}
+namespace tpe {
+#endif
+
+#ifdef TPE_REREAD2
+}  // namespace tpe
+extern "C" int tpe_debug_reread2(unsigned long long *cnt, double *ex, int reset) {
+  if (reset) {
+    unsigned long long z[4] = {0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(tpe::g_rr2_cnt), z, sizeof(z)) == hipSuccess ? 0 : -5;
+  }
+  if (hipMemcpyFromSymbol(cnt, HIP_SYMBOL(tpe::g_rr2_cnt), sizeof(tpe::g_rr2_cnt)) != hipSuccess) return -5;
+  return hipMemcpyFromSymbol(ex, HIP_SYMBOL(tpe::g_rr2_ex), sizeof(tpe::g_rr2_ex)) == hipSuccess ? 0 : -5;
 }
 namespace tpe {
 #endif
