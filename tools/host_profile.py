@@ -42,6 +42,7 @@ def main(cfg='cfg2', n=200):
     cProfile.runctx('loop()', globals(), locals(), '/tmp/host.prof')
     print('per iteration ms (profiled)', 1e3 * (time.perf_counter() - t0) / n)
     pstats.Stats('/tmp/host.prof').sort_stats('tottime').print_stats(25)
+    pstats.Stats('/tmp/host.prof').sort_stats('cumulative').print_stats(40)
 
 
 if __name__ == '__main__':
