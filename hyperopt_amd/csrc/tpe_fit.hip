@@ -337,7 +337,8 @@ __device__ __forceinline__ bool merge_sort_packed(const uint64_t *keys, int n, i
     const int e = u * kFitThreads + t;
     // padding (e >= n): all-ones key bits, position e > every real position
     uint64_t w = (e < n ? ((keys[e] >> shift) << 32) : 0xFFFFFFFF00000000ull) | (uint64_t)e;
-    wave_bitonic64_packed(w);
+    // (a wave-row of padding only is in order already: no network)
+    if (u * kFitThreads + (t & ~63) < n) wave_bitonic64_packed(w);
     k[u] = (uint32_t)(w >> 32);
     p[u] = (uint32_t)w;
     kb0[e] = k[u];
@@ -369,7 +370,11 @@ __device__ __forceinline__ bool merge_sort_packed(const uint64_t *keys, int n, i
       // is not searched: an element of a later run (padding too) ranks after
       // all of it, any other after none of it (runs of a skipped u hold no
       // data, and are only ever such runs)
-      const bool s1 = qb + j1 * len < n, s2 = qb + j2 * len < n, s3 = qb + j3 * len < n;
+      // padding (position >= n) sorts after every real element and in position
+      // order among itself: it keeps its place, e, in every level (no search)
+      const bool pad = p[u] >= (uint32_t)n;
+      const bool s1 = !pad && qb + j1 * len < n, s2 = !pad && qb + j2 * len < n,
+                 s3 = !pad && qb + j3 * len < n;
       int i1 = 0, i2 = 0, i3 = 0;
 #pragma unroll
       for (int step = len / 2; step > 0; step >>= 1) {
@@ -380,7 +385,7 @@ __device__ __forceinline__ bool merge_sort_packed(const uint64_t *keys, int n, i
       i1 = s1 ? i1 + (((uint64_t)o1[i1] < x1) ? 1 : 0) : (j1 < r ? len : 0);
       i2 = s2 ? i2 + (((uint64_t)o2[i2] < x2) ? 1 : 0) : (j2 < r ? len : 0);
       i3 = s3 ? i3 + (((uint64_t)o3[i3] < x3) ? 1 : 0) : (j3 < r ? len : 0);
-      const int dst = qb + (e & (len - 1)) + i1 + i2 + i3;
+      const int dst = pad ? e : qb + (e & (len - 1)) + i1 + i2 + i3;
       dk[dst] = k[u];
       dp[dst] = (uint16_t)p[u];
     }
