@@ -107,13 +107,24 @@ __device__ __forceinline__ bool kp_less(uint64_t ka, uint32_t pa, uint64_t kb, u
 
 // numpy argmax order over (score, global index): a NaN wins at its first
 // index, otherwise the larger score, ties to the lower index (tpe.py:756).
+// (branch-free: the callers take their records with selects, so no
+// exec-masked branch carries a winner's value -- DESIGN §3, the finalize
+// re-read build whose branchy select handed a row-1 winner the row-0 value)
 __device__ __forceinline__ bool better(double sa, int64_t ia, double sb, int64_t ib) {
-  if (ia < 0) return false;
-  if (ib < 0) return true;
   const bool na = sa != sa, nb = sb != sb;
-  if (na || nb) return (na && nb) ? ia < ib : na;
-  if (sa != sb) return sa > sb;
-  return ia < ib;
+  const bool lt = ia < ib;
+  const bool by_score = (sa != sb) ? (sa > sb) : lt;    // neither NaN
+  const bool by_nan = (na && nb) ? lt : na;             // a NaN ranks first
+  return (ia >= 0) & ((ib < 0) | ((na | nb) ? by_nan : by_score));
+}
+
+// a <- (sb, vb, ib) when that record is better (numpy argmax order), by selects
+__device__ __forceinline__ void take_better(double &s, double &v, int64_t &i, double os, double ov,
+                                            int64_t oi) {
+  const bool b = better(os, oi, s, i);
+  s = b ? os : s;
+  v = b ? ov : v;
+  i = b ? oi : i;
 }
 
 __device__ __forceinline__ void wave_best(double &s, double &v, int64_t &i) {
@@ -122,7 +133,7 @@ __device__ __forceinline__ void wave_best(double &s, double &v, int64_t &i) {
     const double os = __shfl_xor(s, o, 64);
     const double ov = __shfl_xor(v, o, 64);
     const int64_t oi = __shfl_xor(i, o, 64);
-    if (better(os, oi, s, i)) { s = os; v = ov; i = oi; }
+    take_better(s, v, i, os, ov, oi);
   }
 }
 

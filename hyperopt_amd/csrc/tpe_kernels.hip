@@ -181,7 +181,7 @@ __global__ __launch_bounds__(64) void k_merge(const int32_t *__restrict__ level_
   for (int r = threadIdx.x; r < world; r += 64) {
     const Partial q = g[((int64_t)r * n_suggest + s) * n_hp + hp];
     active |= q.active;
-    if (better(q.score, q.index, bs_, bi_)) { bs_ = q.score; bv_ = q.value; bi_ = q.index; }
+    take_better(bs_, bv_, bi_, q.score, q.value, q.index);
   }
   wave_best(bs_, bv_, bi_);
 #pragma unroll

@@ -1159,12 +1159,14 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
     if (A.out_la) A.out_la[lo] = lpa;
     if constexpr (!LSE) sc = lpb - lpa;
     const int64_t gi = A.cand_begin + lo;
+#ifdef TPE_REREAD
     if (better(sc, gi, best_s, best_i)) {
       best_s = sc; best_v = x[r]; best_i = gi;
-#ifdef TPE_REREAD
       best_li = li[r];
-#endif
     }
+#else
+    take_better(best_s, best_v, best_i, sc, x[r], gi);
+#endif
   }
 #ifdef TPE_REREAD
   // the same reduction carrying the winner's bucketed slot, plus the slot a
@@ -1260,7 +1262,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
 #ifdef TPE_REREAD
     if (better(qs, qi, fs, fi)) { fs = qs; fv = qv; fi = qi; ft = i; }
 #else
-    if (better(qs, qi, fs, fi)) { fs = qs; fv = qv; fi = qi; }
+    take_better(fs, fv, fi, qs, qv, qi);
 #endif
   }
 #ifdef TPE_REREAD

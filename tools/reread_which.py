@@ -27,6 +27,8 @@ def main():
     plan.fit()
     n, seed = 10_000_000, 7
     r = plan.suggest([seed], n)[0]
+    off = sum(1 for i in range(len(hps)) if _regen(plan, hps, i, seed, r['index'][i]) != r['value'][i])
+    print('config 4 seed %d: %d of %d winners off the draw at their index' % (seed, off, len(hps)))
     shown = 0
     for i in range(len(hps)):
         d = _regen(plan, hps, i, seed, r['index'][i])
