@@ -289,3 +289,32 @@ def test_qlgmm_sampler_matches_lpdf(eng, q, bounds):
             obs_b, exp_b = np.append(obs_b, rest_o), np.append(exp_b, rest_e)
         exp_b = exp_b * obs_b.sum() / exp_b.sum()
         assert chisquare(obs_b, exp_b).pvalue > 1e-4, (q, bounds)
+
+
+def test_score_argmax_numpy_semantics(eng):
+    """broadcast_best's numpy argmax (tpe.py:749-759) through the fused
+    operator: the first of tied maxima wins, a NaN score ranks above every
+    number (the first NaN wins), across the lanes, waves, tiles and the
+    last-tile merge (5000 candidates span several scoring tiles)."""
+    from hyperopt_amd._engine import GMM, LGMM
+    below = ([0.5, 0.5], [0.5, 2.0], [0.3, 0.4])
+    above = ([0.5, 0.5], [-1.0, 4.0], [0.5, 0.6])
+    rng = np.random.RandomState(11)
+    for fam, lo in ((GMM, -3.0), (LGMM, 0.05)):
+        x = rng.uniform(lo, 3.0, 5000) if fam == GMM else np.exp(rng.uniform(-3.0, 1.0, 5000))
+        lb, la, bi, bs = eng.score(fam, x, below, above)
+        ei = lb - la
+        best = int(np.argmax(ei))
+        # a copy of the winner later and earlier: the earliest copy wins
+        for pos in (best + 3 if best + 3 < x.size else best - 3, 17, 4321):
+            y = x.copy()
+            y[pos] = x[best]
+            _, _, bj, _ = eng.score(fam, y, below, above)
+            assert bj == min(pos, best), (fam, pos, best, bj)
+        # NaN candidates: the first NaN is numpy's argmax
+        y = x.copy()
+        y[[2999, 1500, 4100]] = np.nan
+        lb2, la2, bj, bs2 = eng.score(fam, y, below, above)
+        with np.errstate(invalid='ignore'):
+            assert bj == int(np.argmax(lb2 - la2)) == 1500, (fam, bj)
+        assert np.isnan(bs2)
