@@ -524,3 +524,31 @@ print('hex', res.view(np.uint8).tobytes().hex())
     lb = int(b.split('launches ')[1].split()[0])
     assert la >= 3 and lb == 1, (la, lb)
     assert a.split('hex ')[1].strip() == b.split('hex ')[1].strip()
+
+
+def test_sorted_wave_tiles_argmax_numpy_semantics():
+    """The production large-draw form (value-bucketed blocks, wave tiles,
+    prune mode 3) returns numpy's argmax of its own lpdf difference
+    (tpe.py:749-759): over 3e5 candidates of a GMM and an LGMM hp the index
+    is argmax(lb - la) of the returned lpdfs, and with NaN candidates it is
+    the first NaN (every NaN wave falls back to the exact loop; the record
+    selects are branch-free)."""
+    import bench
+    dom, losses, vals, act = bench.build_workload('cfg2')
+    hps, conds, pprior = dom.space.engine_tables()
+    plan = E.Plan(E.default_engine(), hps, conds, pprior, max_trials=losses.size)
+    plan.set_history(losses, vals, act)
+    plan.fit()
+    rng = np.random.RandomState(5)
+    for lab in ('u0', 'lu0'):
+        h = dom.space.by_label[lab]
+        x = rng.uniform(-5, 5, 300_000) if lab == 'u0' else np.exp(rng.uniform(-6.9, 2.3, 300_000))
+        lb, la, bi, bs = plan.score_candidates(h.index, x, sorted_mode=3)
+        assert bi == int(np.argmax(lb - la)), (lab, bi)
+        assert bs == (lb - la)[bi]
+        y = x.copy()
+        y[[250_001, 77_777, 123_456]] = np.nan
+        lb, la, bi, bs = plan.score_candidates(h.index, y, sorted_mode=3)
+        with np.errstate(invalid='ignore'):
+            assert bi == int(np.argmax(lb - la)) == 77_777, (lab, bi)
+        assert np.isnan(bs)
