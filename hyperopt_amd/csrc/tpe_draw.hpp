@@ -224,14 +224,20 @@ __device__ __forceinline__ double erfcinv_fast(double y) {
   return p * (1.0 - y);
 }
 
+// the first Philox block of draw (seed, gi, stream): computed by the caller,
+// where the key (the suggestion's seed) is wave-uniform and its round
+// schedule stays in scalar registers
+__device__ __forceinline__ U4 draw_block0(uint64_t seed, uint64_t gi, uint32_t stream) {
+  return philox(U4{(uint32_t)gi, (uint32_t)(gi >> 32), stream, 0u}, (uint32_t)seed,
+                (uint32_t)(seed >> 32));
+}
+
+// (r0: the words of draw4's first Philox block, draw_block0: u0 picks, u1
+// inverts; the second block -- u2 -- only for the unbounded Box-Muller)
 template <int CAP>
-__device__ double draw_table(const tpe_hp &H, int K, const double *__restrict__ mu,
-                             const double *__restrict__ sg, const DrawTableT<CAP> &T,
-                             uint64_t seed, uint64_t gi, uint32_t stream) {
-  // (the words of draw4's first Philox block: u0 picks, u1 inverts; the
-  // second block -- u2 -- only for the unbounded Box-Muller)
-  const U4 c0{(uint32_t)gi, (uint32_t)(gi >> 32), stream, 0u};
-  const U4 r0 = philox(c0, (uint32_t)seed, (uint32_t)(seed >> 32));
+__device__ double draw_table_from(const tpe_hp &H, int K, const double *__restrict__ mu,
+                                  const double *__restrict__ sg, const DrawTableT<CAP> &T,
+                                  U4 r0, uint64_t seed, uint64_t gi, uint32_t stream) {
   const double u0 = u53(r0.x, r0.y), u1 = u53(r0.z, r0.w);
   const int k = pick_cdf(T.cdf, K, u0);
   if (H.family == TPE_CAT) return (double)k;
@@ -260,6 +266,12 @@ __device__ double draw_table(const tpe_hp &H, int K, const double *__restrict__ 
   if (H.flags & TPE_HAS_Q) x = rint(x / H.q) * H.q;
   return x;
 }
+template <int CAP>
+__device__ double draw_table(const tpe_hp &H, int K, const double *__restrict__ mu,
+                             const double *__restrict__ sg, const DrawTableT<CAP> &T,
+                             uint64_t seed, uint64_t gi, uint32_t stream) {
+  return draw_table_from(H, K, mu, sg, T, draw_block0(seed, gi, stream), seed, gi, stream);
+}
 
 // s is wave-uniform: select the inline seed with an unrolled compare chain
 // (a dynamic index into the by-value argument would copy it to scratch)
@@ -277,9 +289,10 @@ __device__ __forceinline__ uint64_t suggestion_seed(const ScoreArgs &A, int s) {
 template <int CAP>
 __device__ __attribute__((noinline)) double draw_table_ool(const tpe_hp *Hp, int K,
                                                           const double *mu, const double *sg,
-                                                          const DrawTableT<CAP> *T, uint64_t seed,
-                                                          uint64_t gi, uint32_t stream) {
-  return draw_table(*Hp, K, mu, sg, *T, seed, gi, stream);
+                                                          const DrawTableT<CAP> *T, U4 r0,
+                                                          uint64_t seed, uint64_t gi,
+                                                          uint32_t stream) {
+  return draw_table_from(*Hp, K, mu, sg, *T, r0, seed, gi, stream);
 }
 
 // the per-draw rejection sampler, out of line (small register footprint for
@@ -367,8 +380,9 @@ __device__ void draw_block(const ScoreArgs &A, int bx, int row, int s, DrawTable
   double *out = const_cast<double *>(A.cand) + (int64_t)s * A.cand_sstride + (int64_t)slot * A.n_cand;
 #pragma unroll 1
   for (int64_t li = (int64_t)bx * blockDim.x + threadIdx.x; li < A.n_cand; li += stride)
-    out[li] = tab ? draw_table_ool<CAP>(A.hps + hp, K, bmu, bsg, &T, seed,
-                                        (uint64_t)(A.cand_begin + li), (uint32_t)hp)
+    out[li] = tab ? draw_table_ool<CAP>(A.hps + hp, K, bmu, bsg, &T,
+                                        draw_block0(seed, (uint64_t)(A.cand_begin + li), (uint32_t)hp),
+                                        seed, (uint64_t)(A.cand_begin + li), (uint32_t)hp)
                   : draw_one_ool(A.hps + hp, A.info + sb, bw, bmu, bsg, seed,
                                  (uint64_t)(A.cand_begin + li), (uint32_t)hp);
 }
@@ -505,7 +519,8 @@ __device__ __forceinline__ void sorted_block_body(const ScoreArgs &A, int slot, 
       (void)gi; (void)seed; (void)bw;
       x = src[(int64_t)slot * A.n_cand + base + i];
     } else {
-      x = tab ? draw_table_ool<CAP>(A.hps + hp, K, bmu, bsg, &L.T, seed, gi, (uint32_t)hp)
+      x = tab ? draw_table_ool<CAP>(A.hps + hp, K, bmu, bsg, &L.T,
+                                    draw_block0(seed, gi, (uint32_t)hp), seed, gi, (uint32_t)hp)
               : draw_one_ool(A.hps + hp, A.info + sb, bw, bmu, bsg, seed, gi, (uint32_t)hp);
     }
     if (!bucket) {
