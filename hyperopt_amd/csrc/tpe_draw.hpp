@@ -431,12 +431,12 @@ __device__ __forceinline__ void stable_bucket_scatter(const unsigned char *bk, i
   int *mine = cnt + w * 256;
   for (int b = lane; b < 256; b += 64) mine[b] = 0;
   // (a wave's LDS ops complete in order: no barrier between its own rows)
+  // counts: one LDS atomic per element into the wave's own bins (the order
+  // of the adds does not matter; the ranks below keep the scatter stable)
   for (int base = r0; base < r1; base += 64) {
     const int i = base + lane;
-    const bool v = i < r1;
-    const uint32_t d = v ? bk[i] : 0u;
-    const uint64_t mt = lanes_equal8(d, v);
-    if (v && lane == __ffsll((long long)mt) - 1) mine[d] += __popcll(mt);
+    if (i < r1)
+      __hip_atomic_fetch_add(&mine[bk[i]], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   __syncthreads();
   // bucket b (thread b of the first 256): its total over the waves, a block
