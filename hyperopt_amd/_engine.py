@@ -485,21 +485,23 @@ class Plan(object):
                                          0 if host else 1, stream))
         return res
 
-    def score_candidates(self, hp, x, sorted_mode=None):
+    def score_candidates(self, hp, x, sorted_mode=None, want_llik=True):
         """Below / above lpdf and argmax of given candidates of one hp with
         the fitted mixtures.  sorted_mode None: each candidate scored on its
-        own (exact sums); 0 / 1 / 2: the large-draw production form
+        own (exact sums); 0 / 1 / 2 / 3: the large-draw production form
         (tpe_plan_score_candidates_sorted: value-bucketed blocks, log-sum-exp
-        prune mode 0 / 1 / 2)."""
+        prune mode 0 / 1 / 2 / 3).  want_llik False: no lpdf outputs -- the
+        scorer then takes the suggest's EI-only finalize (one log2 of the
+        ratio of the two sums) and (None, None, index, score) is returned."""
         e = self.engine
         x = _f64(x).ravel()
-        lb, la = np.empty(x.size), np.empty(x.size)
+        lb, la = (np.empty(x.size), np.empty(x.size)) if want_llik else (None, None)
         bi, bs = C.c_int64(-1), C.c_double(np.nan)
         mode = -1 if sorted_mode is None else int(sorted_mode)
         with e.lock:
-            e.check(e.lib.tpe_plan_score_candidates_sorted(self.p, int(hp), mode, _dp(x), x.size,
-                                                           _dp(lb), _dp(la), C.byref(bi),
-                                                           C.byref(bs)))
+            e.check(e.lib.tpe_plan_score_candidates_sorted(
+                self.p, int(hp), mode, _dp(x), x.size, _dp(lb) if want_llik else None,
+                _dp(la) if want_llik else None, C.byref(bi), C.byref(bs)))
         return lb, la, bi.value, bs.value
 
     def profile(self, capacity):

@@ -684,17 +684,33 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
       CKH(hipEventRecord(p->ev_fork, st));
       CKH(hipStreamWaitEvent(sl, p->ev_fork, 0));
     }
-    tpe_plan::Prof *pr = nullptr;
-    if (p->prof_cap > 0 && p->prof[1].n < p->prof_cap) pr = &p->prof[1];
-    if (pr) CKH(hipEventRecord(pr->a[pr->n], sl));
-    CKH(launch_lattice(la, p->levels[level].data(), p->hps.data(), p->lat.data(), n_lat,
-                       p->d_lat, sl, lat_rows));
-    if (pr) {
-      CKH(hipEventRecord(pr->b[pr->n], sl));
-      pr->pairs[pr->n] = (double)level;
-      pr->n++;
+    // everything after the fork: a failure still records the join event on
+    // the side stream and waits on it from st, so a captured graph is never
+    // left forked (the chunk loop below joins on its own exits likewise)
+    auto lattice = [&]() -> int {
+      tpe_plan::Prof *pr = nullptr;
+      if (p->prof_cap > 0 && p->prof[1].n < p->prof_cap) pr = &p->prof[1];
+      if (pr) CKH(hipEventRecord(pr->a[pr->n], sl));
+      CKH(launch_lattice(la, p->levels[level].data(), p->hps.data(), p->lat.data(), n_lat,
+                         p->d_lat, sl, lat_rows));
+      if (pr) {
+        CKH(hipEventRecord(pr->b[pr->n], sl));
+        pr->pairs[pr->n] = (double)level;
+        pr->n++;
+      }
+      return TPE_OK;
+    };
+    const int lrc = lattice();
+    if (lat_side) {
+      const hipError_t e1 = hipEventRecord(p->ev_join[0], sl);
+      if (lrc) {
+        if (e1 == hipSuccess) (void)hipStreamWaitEvent(st, p->ev_join[0], 0);
+        return lrc;
+      }
+      if (e1 != hipSuccess) return fail(h, TPE_E_HIP, "lattice side stream join event");
+    } else if (lrc) {
+      return lrc;
     }
-    if (lat_side) CKH(hipEventRecord(p->ev_join[0], sl));
   }
   bool joined = !lat_side;
   // log-sum-exp tiles: two candidate rows per lane, unless that leaves fewer

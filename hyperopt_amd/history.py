@@ -27,9 +27,6 @@ import weakref
 
 import numpy as np
 
-_PENDING_RECHECK = 64   # re-read the losses of up to this many +inf rows per sync
-
-
 def _loss_of(domain, doc):
     v = domain.loss(doc['result'], doc['spec'])
     return math.inf if v is None else float(v)
@@ -180,23 +177,24 @@ class TrialHistory(object):
                 self._loss_dirty = min(self._loss_dirty, r)
             self._put_row(r, tid, loss, v, a, doc)
         # safety net for results mutated in place (no journal entry): the
-        # losses of the few rows still waiting for one are re-read, and those
-        # of the few documents the last rebuild left out (a NaN loss that is
-        # now a number, a duplicate tid whose loss now wins the dedupe)
-        if len(self._dropped) <= _PENDING_RECHECK:
-            for d, l0 in self._dropped.values():
-                loss = _loss_of(dom, d)
-                if not (loss == l0 or (loss != loss and l0 != l0)):
-                    return False
-        if len(self._pending) <= _PENDING_RECHECK:
-            for r in list(self._pending):
-                loss = _loss_of(dom, self.docs[r])
-                if loss != loss:
-                    return False
-                if loss != math.inf:
-                    self.losses[r] = loss
-                    self._pending.discard(r)
-                    self._loss_dirty = min(self._loss_dirty, r)
+        # losses of every row still waiting for one (+inf) are re-read, and
+        # those of every document the last rebuild left out (a NaN loss that
+        # is now a number, a duplicate tid whose loss now wins the dedupe) --
+        # all of them, however many: the reference re-reads every document on
+        # every call (tpe.py:820-848), so a skipped check would be a silent
+        # divergence; the cost is one loss lookup per such document
+        for d, l0 in self._dropped.values():
+            loss = _loss_of(dom, d)
+            if not (loss == l0 or (loss != loss and l0 != l0)):
+                return False
+        for r in list(self._pending):
+            loss = _loss_of(dom, self.docs[r])
+            if loss != loss:
+                return False
+            if loss != math.inf:
+                self.losses[r] = loss
+                self._pending.discard(r)
+                self._loss_dirty = min(self._loss_dirty, r)
         new = view[self._seen:]
         self._grow(self.n + len(new))
         last = self.tids[-1] if self.tids else None

@@ -352,3 +352,34 @@ def test_dropped_document_mutated_in_place_enters_history():
     t.trials[1]['result']['loss'] = 0.25          # in place: no journal entry
     check(dom, t, hist, plan)
     assert hist.tids == [0, 1, 2]
+
+
+def test_many_dropped_and_pending_documents_mutated_in_place():
+    """more than 64 dropped documents (NaN losses) and more than
+    64 pending (+inf) rows, each result then changed in place (no journal
+    entry): every one enters the incrementally synced history with its new
+    loss, as the reference's per-call reassembly would have it."""
+    dom = Domain(lambda x: 0, SPACE)
+    t = Trials()
+    hist = TrialHistory(dom)
+    plan = FakePlan(len(dom.space.labels), 512)
+    n = 300
+    t.insert_trial_docs(rand.suggest(list(range(n)), dom, t, 5))
+    t.refresh()
+    for i, d in enumerate(t.trials):
+        if i % 3 == 0:
+            d['result'] = {'status': 'ok', 'loss': float('nan')}     # dropped (100)
+            d['state'] = H.JOB_STATE_DONE
+        elif i % 3 == 1:
+            d['result'] = {'status': 'ok', 'loss': float(i)}
+            d['state'] = H.JOB_STATE_DONE
+        # i % 3 == 2: left NEW, loss +inf (pending, 100 rows)
+    check(dom, t, hist, plan)
+    assert len(hist._dropped) == 100 and len(hist._pending) == 100
+    for i, d in enumerate(t.trials):
+        if i % 3 != 1:
+            d['result']['loss'] = 0.5 * i               # in place: no journal entry
+    check(dom, t, hist, plan)
+    assert hist.tids == list(range(n))
+    assert np.array_equal(hist.losses[:n], [0.5 * i if i % 3 != 1 else float(i)
+                                            for i in range(n)])
