@@ -445,7 +445,7 @@ def main():
     plan.census(True)
     for i in range(n_prof):
         step(args.warmup + args.steps + n_prof + i)
-    census = plan.census(False, n=9)
+    census = plan.census(False, n=10)
 
     e2e = None
     if rank == 0 and world == 1 and not args.no_e2e:
@@ -483,18 +483,21 @@ def report(args, C, eng, world, mode, elapsed, value, pairs_step, pairs_suggest,
     lse_peak_exact = eng.microbench(3)
     lse_peak_shift = eng.microbench(6 if args.prune == 3 else 5)
     lse_peak_exact32 = eng.microbench(7)   # mode 3's fp32 per-group-lift pair
-    lse_peak = max(lse_peak_exact, lse_peak_shift)
+    lse_peak_mom = eng.microbench(8)       # mode 3's moment form of a 16-component chunk
+    lse_peak = max(lse_peak_exact, lse_peak_shift, lse_peak_mom if args.prune == 3 else 0.0)
     erf_peak = eng.microbench(4)
     lse_pairs = kinds.get('lse_gmm', 0.0) + kinds.get('lse_lgmm', 0.0)
     per_launch = max(1, launches)
     lse_exec = census[5] / per_launch if census[3] else lse_pairs
     lse_shift = census[4] / per_launch if census[3] else 0.0   # of which one-exponent form
     lse_exact32 = census[6] / per_launch if census[3] else 0.0  # fp32 per-group-lift form
+    lse_mom = census[9] / per_launch if census[3] else 0.0      # of lse_shift: moment form
     erf_exec = census[2] / per_launch
     t_kernel = score_ms * 1e-3
     # each evaluated pair priced at the register-only rate of the arithmetic
     # it ran: per-group-max lift, one wave exponent, or quantized erf
-    t_peak = ((lse_exec - lse_shift - lse_exact32) / lse_peak_exact + lse_shift / lse_peak_shift +
+    t_peak = ((lse_exec - lse_shift - lse_exact32) / lse_peak_exact +
+              (lse_shift - lse_mom) / lse_peak_shift + lse_mom / lse_peak_mom +
               lse_exact32 / lse_peak_exact32 + erf_exec / erf_peak)
     frac = t_peak / t_kernel if t_kernel else None
     achieved = (frac or 0.0) * lse_peak
@@ -520,8 +523,12 @@ def report(args, C, eng, world, mode, elapsed, value, pairs_step, pairs_suggest,
                      'SURVEY 8d "1 exp + 6 flops"; prune mode 3 one-exponent pair: 1 packed '
                      'fp32 FMA pair per 2 components + v_exp_f32 + sums; mode 3 per-group-lift '
                      'pair below the one-exponent size: the same in fp32 with the group max and '
-                     'lift; quantized pair: 2 OCML fp64 erf + 8 flops)',
+                     'lift; mode 3 moment form of a 16-component equal-sigma chunk: one exp2 + '
+                     'a degree-9 packed fp32 polynomial per candidate and chunk, 16 pairs; '
+                     'quantized pair: 2 OCML fp64 erf + 8 flops)',
                 lse_evaluated_shifted_pairs_per_launch=lse_shift,
+                lse_evaluated_moment_pairs_per_launch=lse_mom,
+                lse_pair_moment_peak_per_s=lse_peak_mom,
                 lse_shifted_retry_pairs_per_launch=census[7] / per_launch,
                 lse_shifted_wide_block_pairs_per_launch=census[8] / per_launch,
                 lse_evaluated_exact_f32_pairs_per_launch=lse_exact32,

@@ -36,6 +36,7 @@ EXPORTS = (
     'tpe_synchronize', 'tpe_split', 'tpe_parzen_fit', 'tpe_categorical_posterior',
     'tpe_lpdf', 'tpe_score', 'tpe_sample', 'tpe_plan_create', 'tpe_plan_destroy',
     'tpe_plan_num_levels', 'tpe_plan_set_history', 'tpe_plan_fit', 'tpe_plan_get_mixture',
+    'tpe_plan_get_table',
     'tpe_plan_suggest', 'tpe_plan_merge', 'tpe_plan_score_candidates', 'tpe_plan_last_stats',
     'tpe_plan_profile', 'tpe_plan_profile_read', 'tpe_microbench', 'tpe_plan_get_results',
     'tpe_plan_results_device', 'tpe_plan_census', 'tpe_plan_fit_suggest',
@@ -137,6 +138,7 @@ def load_library(path: str = LIB_PATH):
                                                   vp]),
             'tpe_plan_fit': (C.c_int, [vp, dbl, i32, dbl, i32, vp]),
             'tpe_plan_get_mixture': (C.c_int, [vp, i32, i32, _D, _D, _D, i64, C.POINTER(i64)]),
+            'tpe_plan_get_table': (C.c_int, [vp, i32, i32, i32, vp, i64, C.POINTER(i64)]),
             'tpe_plan_suggest': (C.c_int, [vp, C.POINTER(u64), i64, i64, i64, i32, vp, i32, vp]),
             'tpe_plan_fit_suggest': (C.c_int, [vp, dbl, i32, dbl, i32, C.POINTER(u64), i64, i64,
                                                vp, i32, vp]),
@@ -418,6 +420,19 @@ class Plan(object):
         k = k.value
         return w[:k].copy(), mu[:k].copy(), sg[:k].copy()
 
+    def table(self, hp, side=0, which=2):
+        """Raw scoring table of slot (hp, side) as bytes (tpe_plan_get_table:
+        0 coefficients, 1 block-local fp32, 2 moment chunks; diagnostics)."""
+        e = self.engine
+        n = C.c_int64(0)
+        with e.lock:
+            e.check(e.lib.tpe_plan_get_table(self.p, int(hp), int(side), int(which), None, 0,
+                                             C.byref(n)))
+            buf = np.empty(n.value, dtype=np.uint8)
+            e.check(e.lib.tpe_plan_get_table(self.p, int(hp), int(side), int(which),
+                                             buf.ctypes.data, buf.size, C.byref(n)))
+        return buf
+
     def suggest(self, seeds, n_cand, cand_begin=0, level=-1, out=None, stream=None, fetch=True):
         """Returns a structured array [n_suggest, n_hp] of RESULT_DTYPE (host)
         unless ``out`` is a device pointer (int) or ``fetch`` is False (the
@@ -539,10 +554,11 @@ class Plan(object):
         log-sum-exp total, log-sum-exp evaluated in the one-exponent form,
         log-sum-exp evaluated, of those in the fp32 per-group-lift form[,
         one-exponent pairs re-evaluated by a wave's second attempt,
-        one-exponent pairs of wide blocks (mode 3's fp64 loop)]) -- the first
-        ``n`` (7 or 9); enable it for the following suggests."""
+        one-exponent pairs of wide blocks (mode 3's fp64 loop), one-exponent
+        pairs evaluated in the moment form of their chunk]) -- the first ``n``
+        (7, 9 or 10); enable it for the following suggests."""
         e = self.engine
-        out = (C.c_int64 * 9)()
+        out = (C.c_int64 * 10)()
         with e.lock:
             e.check(e.lib.tpe_plan_census_n(self.p, int(bool(enable)), out, int(n)))
         return tuple(int(v) for v in out[:n])

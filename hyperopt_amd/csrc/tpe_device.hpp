@@ -260,4 +260,70 @@ __device__ __forceinline__ void store_lse_envelope(Coef *table, int64_t k, EnvTe
   if (wide) out[3] = -out[3];  // the block keeps the fp64 quadratic in mode 3
 }
 
+// reductions over the 16 lanes of a DPP row (every lane of the row active;
+// xor / mirror steps: every lane ends with the same, bitwise, value)
+__device__ __forceinline__ double row16_min(double v) {
+  v = fmin(v, dppd<kDppXor1>(v));
+  v = fmin(v, dppd<kDppXor2>(v));
+  v = fmin(v, dppd<kDppHalfMirror>(v));
+  return fmin(v, dppd<kDppMirror>(v));
+}
+__device__ __forceinline__ double row16_max(double v) {
+  v = fmax(v, dppd<kDppXor1>(v));
+  v = fmax(v, dppd<kDppXor2>(v));
+  v = fmax(v, dppd<kDppHalfMirror>(v));
+  return fmax(v, dppd<kDppMirror>(v));
+}
+__device__ __forceinline__ double row16_sum(double v) {
+  v += dppd<kDppXor1>(v);
+  v += dppd<kDppXor2>(v);
+  v += dppd<kDppHalfMirror>(v);
+  return v + dppd<kDppMirror>(v);
+}
+
+// The moment form (CoefM, tpe_internal.hpp) of the 16-component chunk held
+// by this lane's DPP row (component k = lane's, k & 15 = its place in the
+// chunk): centre = mu' midpoint, T_k = t_k(centre) = c - a^2 d_k^2,
+// rho_k = 2^(T_k - T*), q_k = 2 a^2 ln2 d_k, m_j = sum_k rho_k q_k^j / j! in
+// fp64, stored fp32.  Eligible only when every valid component has the same
+// a^2 (the same sigma) and the terms are finite; else xh = +inf.
+__device__ __forceinline__ void store_lse_moments(CoefM *tm, int64_t k, EnvTerm e, bool valid) {
+  const double LN2 = 0.6931471805599453;
+  const double lo = row16_min(valid ? e.m : INFINITY), hi = row16_max(valid ? e.m : -INFINITY);
+  const double amin = row16_min(valid ? e.a2 : INFINITY), amax = row16_max(valid ? e.a2 : -INFINITY);
+  const double cen = lo <= hi ? 0.5 * (lo + hi) : 0.0;
+  const double d = valid ? e.m - cen : 0.0;
+  const double T = valid ? e.c - e.a2 * (d * d) : -INFINITY;
+  const double Tm = row16_max(T == T ? T : INFINITY);
+  const double hh = row16_max(valid ? fabs(d) : 0.0);
+  const bool ok = lo <= hi && amin == amax && amin > 0.0 && amin < 1.0e300 && Tm > -1.0e300 &&
+                  Tm < 1.0e300 && hh < 1.0e300;
+  const double rho = (valid && ok) ? exp2(T - Tm) : 0.0;
+  const double q = 2.0 * amin * LN2 * d;
+  float m[kMomDeg + 1];
+  double p = rho, fact = 1.0;
+#pragma unroll
+  for (int j = 0; j <= kMomDeg; ++j) {
+    if (j > 0) fact *= (double)j;
+    m[j] = (float)(row16_sum(p) / fact);
+    p *= q;
+  }
+  if (k % kMomChunk) return;
+  CoefM *b = tm + k / kMomChunk;
+  const double base = ok ? floor(Tm) : 0.0;
+  float xh = INFINITY;
+  if (ok) {
+    const double x = hh * 2.0 * amin * LN2;
+    xh = (float)x;
+    if ((double)xh < x) xh = nextafterf(xh, INFINITY);
+  }
+  b->center = cen;
+  b->xh = xh;
+  b->base = (float)base;
+  b->cm = (float)(Tm - base);
+  b->gam = (float)(-amin);
+#pragma unroll
+  for (int j = 0; j <= kMomDeg; ++j) b->m[j] = m[j];
+}
+
 }  // namespace tpe

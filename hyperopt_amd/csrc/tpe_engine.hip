@@ -21,6 +21,7 @@ using namespace tpe;
 static int lse_shift_min();
 static bool small_sort_on();
 static int64_t chunk_budget();
+static bool moment_on();
 constexpr int64_t kSmallSortMin = 2048;  // candidates per chunk worth bucketing a small draw
 
 struct tpe_engine {
@@ -57,6 +58,7 @@ struct tpe_plan {
   MixInfo *d_info = nullptr;
   Coef *d_coef = nullptr;
   Coef32 *d_coef32 = nullptr;  // [2P][kcap / kCoefBlock] block-local fp32 LSE terms
+  CoefM *d_coefm = nullptr;    // [2P][mom_stride(kcap)] moment form of 16-component chunks
   int64_t n = 0;  // history length
   // suggestion state
   int64_t s_cap = 0;
@@ -174,7 +176,7 @@ void plan_free_buffers(tpe_plan *p) {
                   p->d_losses, p->d_vals, p->d_active, p->d_below, p->d_mw, p->d_mmu,
                   p->d_msig, p->d_scratch, p->d_info, p->d_coef, p->d_results, p->d_seeds,
                   p->d_partial, p->d_ext, p->d_lb, p->d_la, p->d_cand, p->d_cpos,
-                  p->d_ticket, p->d_sortbuf, p->d_census, p->d_lat_info, p->d_lat, p->d_coef32};
+                  p->d_ticket, p->d_sortbuf, p->d_census, p->d_lat_info, p->d_lat, p->d_coef32, p->d_coefm};
   for (void *b : bufs) dfree(b);
   if (p->h_results) (void)hipHostFree(p->h_results);
   p->h_results = nullptr;
@@ -352,6 +354,7 @@ int plan_build(tpe_engine *h, const tpe_space *sp, int64_t max_trials, tpe_plan 
   CKH(hipMemset(p->d_census, 0, kCensus * sizeof(unsigned long long)));
   CKH(dalloc(&p->d_coef, (size_t)slots * kcap));
   CKH(dalloc(&p->d_coef32, (size_t)slots * (kcap / kCoefBlock)));
+  CKH(dalloc(&p->d_coefm, (size_t)slots * mom_stride(kcap)));
   CKH(hipEventCreate(&p->ev0));
   CKH(hipEventCreate(&p->ev1));
   CKH(hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming));
@@ -539,6 +542,7 @@ ScoreArgs base_args(tpe_plan *p, int64_t n_sug) {
   a.info = p->d_info;
   a.coef = p->d_coef;
   a.coef32 = p->d_coef32;
+  a.coefm = p->d_coefm;
   a.mw = p->d_mw;
   a.mmu = p->d_mmu;
   a.msig = p->d_msig;
@@ -552,6 +556,7 @@ ScoreArgs base_args(tpe_plan *p, int64_t n_sug) {
   a.n_suggest = (int32_t)n_sug;
   a.lat_info = p->d_lat_info;
   a.lat = p->d_lat;
+  a.lse_mom = moment_on() ? 1 : 0;
   return a;
 }
 
@@ -573,6 +578,7 @@ FitArgs fit_args(tpe_plan *p, int32_t n_below, double prior_weight, int32_t lf) 
   a.info = p->d_info;
   a.coef = p->d_coef;
   a.coef32 = p->d_coef32;
+  a.coefm = p->d_coefm;
   a.kcap = p->kcap;
   a.ob = p->d_scratch;
   a.tmp = p->d_scratch;
@@ -1135,7 +1141,7 @@ int tpe_score(tpe_handle_t h, int32_t family, const double *x, int64_t n, const 
   if (rc) return rc;
   rc = put_mixture(h, p, 1, wa, ma, sa, ka, kind);
   if (rc) return rc;
-  CKH(launch_prep(p->d_hps, 1, p->d_mw, p->d_mmu, p->d_msig, p->d_info, p->d_coef, p->d_coef32, p->kcap,
+  CKH(launch_prep(p->d_hps, 1, p->d_mw, p->d_mmu, p->d_msig, p->d_info, p->d_coef, p->d_coef32, p->d_coefm, p->kcap,
                   p->d_scratch, h->stream));
   rc = ensure_ext(h, p, n);
   if (rc) return rc;
@@ -1183,7 +1189,7 @@ int tpe_sample(tpe_handle_t h, int32_t family, const double *w, const double *mu
   if (rc) return rc;
   rc = put_mixture(h, p, 1, w, mu, sigma, k, kind);
   if (rc) return rc;
-  CKH(launch_prep(p->d_hps, 1, p->d_mw, p->d_mmu, p->d_msig, p->d_info, p->d_coef, p->d_coef32, p->kcap,
+  CKH(launch_prep(p->d_hps, 1, p->d_mw, p->d_mmu, p->d_msig, p->d_info, p->d_coef, p->d_coef32, p->d_coefm, p->kcap,
                   p->d_scratch, h->stream));
   rc = ensure_ext(h, p, n);
   if (rc) return rc;
@@ -1305,6 +1311,32 @@ int tpe_plan_get_mixture(tpe_plan_t p, int32_t hp, int32_t side, double *w, doub
   if (w) CKH(hipMemcpy(w, p->d_mw + slot * p->kcap, mi.K * 8, hipMemcpyDeviceToHost));
   if (mu) CKH(hipMemcpy(mu, p->d_mmu + slot * p->kcap, mi.K * 8, hipMemcpyDeviceToHost));
   if (sigma) CKH(hipMemcpy(sigma, p->d_msig + slot * p->kcap, mi.K * 8, hipMemcpyDeviceToHost));
+  return TPE_OK;
+}
+
+int tpe_plan_get_table(tpe_plan_t p, int32_t hp, int32_t side, int32_t which, void *out,
+                       int64_t cap_bytes, int64_t *bytes) {
+  if (!p || !bytes) return TPE_E_INVALID;
+  tpe_engine *h = p->eng;
+  if (hp < 0 || hp >= p->P || side < 0 || side > 1 || which < 0 || which > 2)
+    return fail(h, TPE_E_INVALID, "bad hp/side/table");
+  CKH(hipSetDevice(h->device));
+  CKH(hipDeviceSynchronize());
+  const int64_t slot = 2 * (int64_t)hp + side;
+  const void *src = nullptr;
+  if (which == 0) {
+    *bytes = p->kcap * (int64_t)sizeof(Coef);
+    src = p->d_coef + slot * p->kcap;
+  } else if (which == 1) {
+    *bytes = p->kcap / kCoefBlock * (int64_t)sizeof(Coef32);
+    src = p->d_coef32 + slot * (p->kcap / kCoefBlock);
+  } else {
+    *bytes = mom_stride(p->kcap) * (int64_t)sizeof(CoefM);
+    src = p->d_coefm + slot * mom_stride(p->kcap);
+  }
+  if (!out) return TPE_OK;
+  if (*bytes > cap_bytes) return fail(h, TPE_E_INVALID, "capacity too small");
+  CKH(hipMemcpy(out, src, (size_t)*bytes, hipMemcpyDeviceToHost));
   return TPE_OK;
 }
 
@@ -1709,6 +1741,17 @@ static bool small_sort_on() {
   return v;
 }
 
+// the moment form of equal-sigma 16-component chunks in prune mode 3
+// (CoefM; TPE_MOMENT=0 switches it off: A/B and the parity tests' child
+// processes)
+static bool moment_on() {
+  static const bool v = [] {
+    const char *e = std::getenv("TPE_MOMENT");
+    return e && std::atoi(e) != 0;  // (off until verified on the GPU)
+  }();
+  return v;
+}
+
 // candidate buffer per scoring chunk, in doubles (TPE_CHUNK_MB overrides, A/B)
 static int64_t chunk_budget() {
   static const int64_t v = [] {
@@ -1740,7 +1783,7 @@ int tpe_plan_set_prune(tpe_plan_t p, int32_t mode) {
 }
 
 int tpe_microbench(tpe_handle_t h, int32_t which, double *per_second) {
-  if (!h || !per_second || which < 0 || which > 7) return TPE_E_INVALID;
+  if (!h || !per_second || which < 0 || which > 8) return TPE_E_INVALID;
   CKH(hipSetDevice(h->device));
   hipDeviceProp_t prop;
   CKH(hipGetDeviceProperties(&prop, h->device));
@@ -1764,8 +1807,9 @@ int tpe_microbench(tpe_handle_t h, int32_t which, double *per_second) {
   // results per thread-iteration: exp / FMA chains, erf chains, LSE pairs
   // (4 candidates x 8 components), quantized pairs (2 chains), shifted LSE
   // pairs (4 x 8), block-local fp32 one-exponent LSE pairs (4 x 2 blocks of
-  // 8), the fp32 per-group-lift pairs (4 x 8)
-  static const double per_iter[8] = {8.0, 16.0, 4.0, 32.0, 2.0, 32.0, 64.0, 32.0};
+  // 8), the fp32 per-group-lift pairs (4 x 8), moment-form pairs (4 x 2
+  // chunks of 16)
+  static const double per_iter[9] = {8.0, 16.0, 4.0, 32.0, 2.0, 32.0, 64.0, 32.0, 128.0};
   *per_second = 4.0 * blocks * 256.0 * iters * per_iter[which] / (ms * 1e-3);
   return TPE_OK;
 }

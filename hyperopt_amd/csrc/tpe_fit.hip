@@ -808,19 +808,25 @@ __device__ __forceinline__ Split compute_split(const FitArgs &A, const FitCtx &C
 // reduction per 8 components, computed with the coefficients) and the
 // padding components of the last block (alpha = -inf: terms exactly 0).
 // ------------------------------------------------------------------------
-__device__ __forceinline__ void store_table(const tpe_hp &H, Coef *cf, Coef32 *cf32, int K,
-                                            const double *w, const double *mu, const double *sg,
-                                            double pacc, bool quant) {
+__device__ __forceinline__ void store_table(const tpe_hp &H, Coef *cf, Coef32 *cf32, CoefM *cfm,
+                                            int K, const double *w, const double *mu,
+                                            const double *sg, double pacc, bool quant) {
   const int kp = (K + kCoefBlock - 1) / kCoefBlock * kCoefBlock;
+  const int kp16 = (K + kMomChunk - 1) / kMomChunk * kMomChunk;
   // kp and the block size are multiples of 8: the 8 lanes of a block's
-  // components are active together for the shuffles
-  for (int k = threadIdx.x; k < (quant ? K : kp); k += blockDim.x) {
+  // components are active together for the shuffles; kp16 (log-sum-exp):
+  // the 16 lanes of a moment chunk likewise (lanes past kp are padding of
+  // the chunk only, with no coefficient entry)
+  for (int k = threadIdx.x; k < (quant ? K : kp16); k += blockDim.x) {
     EnvTerm e{0.0, 0.0, 0.0};
     const bool real = k < K;
     const Coef c = real ? make_coef(H, w[k], mu[k], sg[k], pacc, &e)
                         : Coef{-INFINITY, 0.0, 0.0, 0.0};
-    store_coef(cf, k, c, quant);
-    if (!quant) store_lse_envelope(cf, k, e, real, c, cf32);
+    if (k < kp) {
+      store_coef(cf, k, c, quant);
+      if (!quant) store_lse_envelope(cf, k, e, real, c, cf32);
+    }
+    if (!quant) store_lse_moments(cfm, k, e, real);
   }
 }
 
@@ -832,10 +838,11 @@ __device__ __forceinline__ void store_table(const tpe_hp &H, Coef *cf, Coef32 *c
 // would put that copy on the scratch stack when the call is not inlined)
 __device__ __forceinline__ void prep_slot(const tpe_hp *Hg, int64_t slot, int K, const double *w, const double *mu,
                           const double *sg, MixInfo *info, Coef *coef, Coef32 *coef32,
-                          int64_t kcap, double *tmp, FitShared &sm) {
+                          CoefM *coefm, int64_t kcap, double *tmp, FitShared &sm) {
   const tpe_hp H = *Hg;
   Coef *cf = coef + slot * kcap;
   Coef32 *cf32 = coef32 + slot * (kcap / kCoefBlock);
+  CoefM *cfm = coefm + slot * mom_stride(kcap);
   const double wsum = block_np_sum(w, K, sm);
   STAMP(7);
   if (H.family == TPE_CAT) {
@@ -862,7 +869,7 @@ __device__ __forceinline__ void prep_slot(const tpe_hp *Hg, int64_t slot, int K,
   }
   STAMP(8);
   const bool quant = (H.flags & TPE_HAS_Q) != 0;
-  store_table(H, cf, cf32, K, w, mu, sg, pacc, quant);
+  store_table(H, cf, cf32, cfm, K, w, mu, sg, pacc, quant);
   if (threadIdx.x == 0) {
     MixInfo mi;
     mi.K = K; mi.kind = quant ? 1 : 0; mi.p_accept = pacc; mi.log_pacc = log(pacc);
@@ -963,9 +970,10 @@ __device__ __forceinline__ void fit_continuous(const FitArgs &A, const FitCtx &C
   const bool quant = (H.flags & TPE_HAS_Q) != 0;
   Coef *cf = A.coef + slot * A.kcap;
   Coef32 *cf32 = A.coef32 + slot * (A.kcap / kCoefBlock);
+  CoefM *cfm = A.coefm + slot * mom_stride(A.kcap);
   if (MIXLDS)
     for (int k = threadIdx.x; k < K; k += blockDim.x) { gw[k] = w[k]; gm[k] = mu[k]; gs[k] = sg[k]; }
-  store_table(H, cf, cf32, K, w, mu, sg, pacc, quant);
+  store_table(H, cf, cf32, cfm, K, w, mu, sg, pacc, quant);
   if (threadIdx.x == 0) {
     MixInfo mi;
     mi.K = K; mi.kind = quant ? 1 : 0; mi.p_accept = pacc; mi.log_pacc = log(pacc);
@@ -1120,7 +1128,7 @@ __device__ __forceinline__ void categorical_tail(const FitArgs &A, FitShared &sm
     sg[c] = 0.0;
   }
   __syncthreads();
-  prep_slot(A.hps + slot / 2, slot, upper, w, mu, sg, A.info, A.coef, A.coef32, A.kcap,
+  prep_slot(A.hps + slot / 2, slot, upper, w, mu, sg, A.info, A.coef, A.coef32, A.coefm, A.kcap,
             A.tmp + slot * A.kcap, sm);
 }
 
@@ -1353,7 +1361,8 @@ __global__ __launch_bounds__(256) void k_prep(const tpe_hp *__restrict__ hps,
                                               const double *__restrict__ mmu,
                                               const double *__restrict__ msig,
                                               MixInfo *__restrict__ info, Coef *__restrict__ coef,
-                                              Coef32 *__restrict__ coef32, int64_t kcap,
+                                              Coef32 *__restrict__ coef32,
+                                              CoefM *__restrict__ coefm, int64_t kcap,
                                               double *__restrict__ scratch) {
   __shared__ FitShared sm;
   const int hp = blockIdx.x, side = blockIdx.y;
@@ -1361,7 +1370,7 @@ __global__ __launch_bounds__(256) void k_prep(const tpe_hp *__restrict__ hps,
   const int K = info[slot].K;
   __syncthreads();
   prep_slot(hps + hp, slot, K, mw + slot * kcap, mmu + slot * kcap, msig + slot * kcap, info, coef,
-            coef32, kcap, scratch + slot * kcap, sm);
+            coef32, coefm, kcap, scratch + slot * kcap, sm);
 }
 
 // ------------------------------------------------------------------------
@@ -1395,9 +1404,10 @@ hipError_t launch_split(const FitArgs &a, uint8_t *below, hipStream_t st) {
 
 hipError_t launch_prep(const tpe_hp *hps, int32_t n_hp, const double *mw, const double *mmu,
                        const double *msig, MixInfo *info, Coef *coef, Coef32 *coef32,
-                       int64_t kcap, double *scratch, hipStream_t st) {
+                       CoefM *coefm, int64_t kcap, double *scratch, hipStream_t st) {
   if (n_hp <= 0) return hipSuccess;
-  k_prep<<<dim3(n_hp, 2), 256, 0, st>>>(hps, mw, mmu, msig, info, coef, coef32, kcap, scratch);
+  k_prep<<<dim3(n_hp, 2), 256, 0, st>>>(hps, mw, mmu, msig, info, coef, coef32, coefm, kcap,
+                                        scratch);
   return hipGetLastError();
 }
 

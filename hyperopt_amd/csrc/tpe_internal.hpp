@@ -93,8 +93,9 @@ constexpr float kLseDeadBase = 26.0f;
 // log-sum-exp total / one-exponent evaluated / evaluated / evaluated in the
 // block-local fp32 per-group-lift form / one-exponent pairs of a wave's
 // second attempt (re-centred exponent) / one-exponent pairs of wide blocks
-// (the fp64 loop of mode 3)
-constexpr int kCensus = 9;
+// (the fp64 loop of mode 3) / one-exponent pairs evaluated in the moment
+// form of their chunk (CoefM)
+constexpr int kCensus = 10;
 
 // Per-component scoring coefficients (make_coef, tpe_device.hpp), 4 fields:
 //   LSE: x = alpha, y = beta, z = gamma (t = alpha + y'(beta + gamma y'))
@@ -143,6 +144,41 @@ struct __attribute__((aligned(128))) Coef32 {
 };
 static_assert(sizeof(Coef32) == 128, "two 64-B scalar loads");
 
+// Moment form of a 16-component chunk (prune mode 3, one-exponent wave
+// tiles).  When the chunk's components share one sigma -- every component
+// whose adaptive-Parzen sigma sits at the prior_sigma / min(100, 1 + N)
+// floor (tpe.py:440-456), the common case of long histories -- its terms at
+// y' = centre + v factor as
+//   sum_k 2^(t_k) = 2^(T* - a^2 v^2) * sum_k rho_k exp(q_k v),
+//   T_k = t_k(centre), T* = max_k T_k, rho_k = 2^(T_k - T*), q_k = 2 a^2 ln2 d_k,
+//   d_k = mu'_k - centre,
+// and exp(q_k v) is its Taylor polynomial of degree kMomDeg: the chunk's 16
+// exponentials become one exp2 and a polynomial in v with the fixed
+// coefficients m_j = sum_k rho_k q_k^j / j!.  Truncation: each term's
+// relative error is <= x^(kMomDeg+1) / (kMomDeg+1)! e^x with x = |v| xh,
+// xh = max_k |q_k|; a wave takes the form for a chunk only while its whole
+// candidate range has x <= kMomXLim (<= 7.1e-9 relative).  xh = +inf marks
+// a chunk whose sigmas differ (or non-finite terms): never taken.
+// (tools/moment_error.py emulates it against the oracle.)  64 B = one
+// scalar load.
+constexpr int kMomChunk = 16;
+constexpr int kMomDeg = 9;
+constexpr float kMomXLim = 0.65f;
+struct __attribute__((aligned(64))) CoefM {
+  double center;   // mu' midpoint of the chunk (fp64)
+  float base;      // integer near T* (A - M is exact)
+  float cm;        // T* - base
+  float gam;       // -a^2 (log2 units), the shared quadratic coefficient
+  float m[kMomDeg + 1];
+  float xh;        // max_k |q_k| (nats per unit v), rounded up; +inf: not eligible
+};
+static_assert(sizeof(CoefM) == 64, "one 64-B scalar load");
+static_assert(kMomChunk == 2 * 8, "a moment chunk is two coefficient blocks");
+// moment-table entries per slot (kcap is a multiple of kCoefBlock)
+__host__ __device__ constexpr int64_t mom_stride(int64_t kcap) {
+  return (kcap + kMomChunk - 1) / kMomChunk;
+}
+
 struct Partial {  // == tpe_result layout
   double score;
   double value;
@@ -179,6 +215,7 @@ struct ScoreArgs {
   const MixInfo *info;       // [2*P]
   const Coef *coef;          // [2*P][kcap]
   const Coef32 *coef32;      // [2*P][kcap / kCoefBlock] block-local fp32 LSE terms
+  const CoefM *coefm;        // [2*P][mom_stride] moment form of 16-component chunks
   const double *mw, *mmu, *msig;  // [2*P][kcap] (sampler reads side 0)
   const uint64_t *seeds;     // [S]
   const double *cand;        // candidates [S][n_slots][n_cand] (drawn or external)
@@ -218,6 +255,8 @@ struct ScoreArgs {
   int32_t lse_shift_min;     // lse_prune 2: smallest mixture (components) for one wave exponent
   int32_t lse_f32;           // unpruned log-sum-exp slots also take the block-local fp32
                              // pairs (prune mode 3's arithmetic on small draws)
+  int32_t lse_mom;           // prune mode 3 wave tiles take the moment form of eligible
+                             // 16-component chunks (CoefM; TPE_MOMENT=0 switches it off)
   const LatInfo *lat_info;   // [P] value lattices (KIND_LAT slots)
   const double2 *lat;        // lattice (lpdf below, lpdf above) pairs
 };
@@ -239,6 +278,7 @@ struct FitArgs {
   MixInfo *info;             // [2P]
   Coef *coef;                // [2P][kcap]
   Coef32 *coef32;            // [2P][kcap / kCoefBlock]
+  CoefM *coefm;              // [2P][mom_stride(kcap)]
   int64_t kcap;
   double *ob;                // [2P][kcap] scratch: observations of the slot
   double *tmp;               // [2P][kcap] scratch (may alias ob)
@@ -256,7 +296,7 @@ bool is_sorted_draw_kernel_fn(const void *f);
 const void *lattice_draw_kernel_fn();      // k_lattice<true> (lattice + fused draw)
 hipError_t launch_prep(const tpe_hp *hps, int32_t n_hp, const double *mw,
                        const double *mmu, const double *msig, MixInfo *info,
-                       Coef *coef, Coef32 *coef32, int64_t kcap, double *scratch,
+                       Coef *coef, Coef32 *coef32, CoefM *coefm, int64_t kcap, double *scratch,
                        hipStream_t st);
 hipError_t launch_score(const ScoreArgs &a, bool has_erf, hipStream_t st);
 // lpdf pairs of every lattice point of the first n_lat hps of a level

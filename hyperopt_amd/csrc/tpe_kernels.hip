@@ -496,6 +496,52 @@ __global__ __launch_bounds__(256) void k_micro(int iters, double *sink) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) acc += sm[c] + m[c];
     if (acc == 12345.0) sink[t] = acc;
+  } else if constexpr (WHICH == 8) {
+    // prune mode 3's moment form (CoefM, lse_chunks_shifted): per (candidate
+    // row pair, 16-component chunk) v = fp32(y' - centre) for both rows,
+    // -a^2 v^2 + offset, a degree-kMomDeg Horner polynomial on packed fp32
+    // pairs, two exp2 and two multiplies, two chunks' sums added in fp32,
+    // then one fp64 add per row; 2 row pairs x 2 chunks = 4 x 2 x 16 pairs
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    double y[4], sm[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) { y[c] = 1e-3 * (t + c); sm[c] = 0.0; }
+    float mm[2][kMomDeg + 1];
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int q = 0; q <= kMomDeg; ++q) mm[b][q] = 1.0f / (1.0f + q + b);
+    const double centre[2] = {0.25, 0.75};
+    float A = 3.0f;
+    const float Mf = 5.0f, gam = -72.0f;
+    for (int i = 0; i < iters; ++i) {
+      const float off = 0.5f + (A - Mf);
+#pragma unroll
+      for (int c = 0; c < 4; c += 2) {
+        float bs[2][2];
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const f2v v = {(float)(y[c] - centre[b]), (float)(y[c + 1] - centre[b])};
+          const f2v arg = __builtin_elementwise_fma(f2v{gam, gam}, v * v, f2v{off, off});
+          f2v p = __builtin_elementwise_fma(f2v{mm[b][kMomDeg], mm[b][kMomDeg]}, v,
+                                            f2v{mm[b][kMomDeg - 1], mm[b][kMomDeg - 1]});
+#pragma unroll
+          for (int q = kMomDeg - 2; q >= 0; --q)
+            p = __builtin_elementwise_fma(p, v, f2v{mm[b][q], mm[b][q]});
+          bs[b][0] = __builtin_amdgcn_exp2f(arg.x) * p.x;
+          bs[b][1] = __builtin_amdgcn_exp2f(arg.y) * p.y;
+        }
+        sm[c] += (double)(bs[0][0] + bs[1][0]);
+        sm[c + 1] += (double)(bs[0][1] + bs[1][1]);
+        y[c] += 1e-9;
+        y[c + 1] += 1e-9;
+      }
+      A += 1e-7f;
+    }
+    double acc = 0.0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc += sm[c];
+    if (acc == 12345.0) sink[t] = acc;
   } else if constexpr (WHICH == 4) {
     // one quantized pair exactly as k_score computes a live one: two OCML
     // fp64 erf, the reference's Phi and two-stage increment; 2 chains
@@ -542,6 +588,7 @@ hipError_t launch_micro(int which, int blocks, int iters, double *sink, hipStrea
     case 5: k_micro<5><<<blocks, 256, 0, st>>>(iters, sink); break;
     case 6: k_micro<6><<<blocks, 256, 0, st>>>(iters, sink); break;
     case 7: k_micro<7><<<blocks, 256, 0, st>>>(iters, sink); break;
+    case 8: k_micro<8><<<blocks, 256, 0, st>>>(iters, sink); break;
     default: k_micro<2><<<blocks, 256, 0, st>>>(iters, sink); break;
   }
   return hipGetLastError();

@@ -140,6 +140,48 @@ __device__ __forceinline__ void load_block32(KC32 *__restrict__ rb, uint32_t j, 
     g.c[q] = b->c[q];
   }
 }
+// The moment form of a 16-component chunk (CoefM, tpe_internal.hpp): one
+// 64-B scalar load per chunk
+typedef const CoefM __attribute__((address_space(4))) KCM;
+__device__ __forceinline__ KCM *uniform_ptrm(const CoefM *p) {
+  const uint64_t u = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  return (KCM *)(((uint64_t)hi << 32) | lo);
+}
+struct MomGroup {
+  double c;
+  float A, cm, g;
+  float m[kMomDeg + 1];
+};
+__device__ __forceinline__ void load_mom(KCM *__restrict__ rb, uint32_t j, MomGroup &g) {
+  KCM *b = rb + j;
+  g.c = b->center;
+  g.A = b->base;
+  g.cm = b->cm;
+  g.g = b->gam;
+#pragma unroll
+  for (int q = 0; q <= kMomDeg; ++q) g.m[q] = b->m[q];
+}
+// a chunk's terms for the two candidate rows of a lane, but the exponential:
+// v = fp32(y' - centre), arg = -a^2 v^2 + (T* - A) + (A - M) (A - M exact),
+// and the degree-kMomDeg polynomial in v by Horner on packed fp32 pairs (the
+// coefficients are scalar operands); the chunk's sum is 2^arg * p
+__device__ __forceinline__ void mom_terms(const MomGroup &g, float Mf, const double (&y)[2],
+                                          f2v &arg, f2v &p) {
+  const float off = g.cm + (g.A - Mf);
+  const f2v v = {(float)(y[0] - g.c), (float)(y[1] - g.c)};
+  arg = __builtin_elementwise_fma(f2v{g.g, g.g}, v * v, f2v{off, off});
+  p = __builtin_elementwise_fma(f2v{g.m[kMomDeg], g.m[kMomDeg]}, v,
+                                f2v{g.m[kMomDeg - 1], g.m[kMomDeg - 1]});
+#pragma unroll
+  for (int q = kMomDeg - 2; q >= 0; --q) p = __builtin_elementwise_fma(p, v, f2v{g.m[q], g.m[q]});
+}
+__device__ __forceinline__ void mom_sum(const f2v &arg, const f2v &p, float (&bs)[2]) {
+  bs[0] = __builtin_amdgcn_exp2f(arg.x) * p.x;
+  bs[1] = __builtin_amdgcn_exp2f(arg.y) * p.y;
+}
+
 // the lowest set bit of m, or 0 when m is empty (the caller then reloads
 // block 0 of the round: a valid address, its values unused)
 __device__ __forceinline__ uint32_t low_bit(uint64_t m) {
@@ -229,6 +271,7 @@ struct LseCensus {
   uint32_t f32;                 // the evaluated ones in the fp32 per-group-lift form
   uint32_t retry;               // one-exponent pairs evaluated again by a second attempt
   uint32_t wide;                // one-exponent pairs of wide blocks (fp64 loop, mode 3)
+  uint32_t mom;                 // one-exponent pairs evaluated in the moment form (CoefM)
 };
 
 // A block's envelope bound over the wave's candidate range [lo, hi]: the
@@ -484,7 +527,8 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
                                                    const Coef *__restrict__ cv, int c0, int nb,
                                                    const double (&y)[KR], const bool (&valid)[KR],
                                                    LseAcc (&out)[KR], LseWindow win, int nvalid,
-                                                   LseCensus &cen, KC32 *__restrict__ c32 = nullptr) {
+                                                   LseCensus &cen, KC32 *__restrict__ c32 = nullptr,
+                                                   const CoefM *__restrict__ cmv = nullptr) {
   const int lane = threadIdx.x & 63;
   const int nch = (nb + kChunk - 1) / kChunk;
   const double *tb = reinterpret_cast<const double *>(cv);
@@ -581,7 +625,70 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
         // order; one bit scan and a 32-bit offset per block (SALU)
         const float Mf = (float)M;  // an integer (< 2^24 in magnitude): exact
         KC32 *rb = c32 + 2 * r0;
-        uint64_t m = __ballot(live && !wide);
+        // chunks in the moment form (CoefM): lane 2i tests chunk r0 + i -- its
+        // sigmas equal and x = |v| xh <= kMomXLim over the wave's whole
+        // candidate range -- and the chunk is taken when either of its two
+        // blocks is live; its blocks then leave the pair and wide loops
+        static_assert(KR == 2, "the moment form packs the lane's two candidate rows");
+        constexpr uint64_t kEven = 0x5555555555555555ull;
+        bool elig = false;
+        if (cmv && has && !(lane & 1)) {
+          const CoefM *q = cmv + (r0 + (lane >> 1));
+          const float cf = (float)q->center;
+          const float x = fmaxf(fabsf(win.lo - cf), fabsf(win.hi - cf)) * q->xh;
+          elig = x <= kMomXLim;
+        }
+        const uint64_t lm = __ballot(live);
+        const uint64_t cmask = (lm | (lm >> 1)) & __ballot(elig) & kEven;
+        const uint64_t cover = cmask | (cmask << 1);
+        if constexpr (CENSUS) {
+          const int n = (cmask >> lane) & 1 ? min(kMomChunk, nb - k0) : 0;
+          uint32_t mx = (uint32_t)n;
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) mx += __shfl_xor(mx, o, 64);
+          // (the chunk's blocks counted as evaluated whether or not both were live)
+          uint32_t lx = (uint32_t)(has && (((cover & ~lm) >> lane) & 1) ? min(kGroup, nb - k0) : 0);
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) lx += __shfl_xor(lx, o, 64);
+          cen.mom += mx * (uint32_t)nvalid;
+          cen.exec += lx * (uint32_t)nvalid;
+          cen.shift += lx * (uint32_t)nvalid;
+        }
+        {
+          KCM *rm = uniform_ptrm(cmv) + r0;
+          uint64_t cm = cmask;
+          bool hm = cm != 0;
+          MomGroup g;
+          if (hm) load_mom(rm, low_bit(cm) >> 1, g);
+          // two chunks per iteration, their fp32 sums added in fp32 and
+          // converted once (as the pair loop below)
+          while (hm) {
+            f2v a0, p0;
+            mom_terms(g, Mf, y, a0, p0);
+            cm &= cm - 1;
+            hm = cm != 0;
+            load_mom(rm, low_bit(cm) >> 1, g);
+            __builtin_amdgcn_sched_barrier(0);
+            float b0[2];
+            mom_sum(a0, p0, b0);
+            if (!hm) {
+#pragma unroll
+              for (int r = 0; r < KR; ++r) s[r] += (double)b0[r];
+              break;
+            }
+            f2v a1, p1;
+            mom_terms(g, Mf, y, a1, p1);
+            cm &= cm - 1;
+            hm = cm != 0;
+            load_mom(rm, low_bit(cm) >> 1, g);
+            __builtin_amdgcn_sched_barrier(0);
+            float b1[2];
+            mom_sum(a1, p1, b1);
+#pragma unroll
+            for (int r = 0; r < KR; ++r) s[r] += (double)(b0[r] + b1[r]);
+          }
+        }
+        uint64_t m = __ballot(live && !wide) & ~cover;
         bool hv = m != 0;
         CoefGroup32 g32;
         if (hv) load_block32(rb, low_bit(m), g32);
@@ -611,7 +718,7 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
 #pragma unroll
           for (int r = 0; r < KR; ++r) s[r] += (double)(b0[r] + b1[r]);
         }
-        uint64_t xk = __ballot(live && wide);
+        uint64_t xk = __ballot(live && wide) & ~cover;
         while (next_live<STRIDE>(xk, r0, kg)) {
           CoefGroup g;
           load_group(cs, kg, g);
@@ -1014,7 +1121,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
     // wave index as a scalar: the component addresses below are wave-uniform,
     // so the coefficients come in through scalar loads (SGPR operands)
     const int wv = __builtin_amdgcn_readfirstlane(wave);
-    LseCensus lcen{0u, 0u, 0u, 0u, 0u, 0u};
+    LseCensus lcen{0u, 0u, 0u, 0u, 0u, 0u, 0u};
     int nvalid = 0;
 #pragma unroll
     for (int r = 0; r < KR; ++r) nvalid += valid[r] ? 1 : 0;
@@ -1041,10 +1148,11 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
         const int cw0 = WT ? 0 : wv;
         bool shifted = false;
         if (prune && A.lse_prune > 1 && K >= A.lse_shift_min && win.thr > -INFINITY) {
-          if (A.lse_prune > 2)  // block-local fp32 pairs (Coef32)
+          if (A.lse_prune > 2)  // block-local fp32 pairs (Coef32), moment chunks (CoefM)
             shifted = lse_chunks_shifted<KR, CENSUS, ST, true>(
                 uniform_ptr(cm), cm, cw0, K, y, valid, lacc[mix], win, nvalid, lcen,
-                uniform_ptr32(A.coef32 + (mix ? sa : sb) * (A.kcap / kCoefBlock)));
+                uniform_ptr32(A.coef32 + (mix ? sa : sb) * (A.kcap / kCoefBlock)),
+                A.lse_mom ? A.coefm + (mix ? sa : sb) * mom_stride(A.kcap) : nullptr);
           else
             shifted = lse_chunks_shifted<KR, CENSUS, ST>(uniform_ptr(cm), cm, cw0, K, y, valid,
                                                          lacc[mix], win, nvalid, lcen);
@@ -1098,10 +1206,10 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
     }
     if constexpr (CENSUS && LSE) {
       // nvalid is per lane: the per-lane sums add up to the wave's pairs
-      unsigned long long c2[6] = {lcen.total, lcen.exec, lcen.shift, lcen.f32, lcen.retry,
-                                  lcen.wide};
+      unsigned long long c2[7] = {lcen.total, lcen.exec, lcen.shift, lcen.f32, lcen.retry,
+                                  lcen.wide, lcen.mom};
 #pragma unroll
-      for (int q = 0; q < 6; ++q) {
+      for (int q = 0; q < 7; ++q) {
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) c2[q] += __shfl_xor(c2[q], o, 64);
       }
@@ -1112,6 +1220,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
         atomicAdd(A.census + 6, c2[3]);
         atomicAdd(A.census + 7, c2[4]);
         atomicAdd(A.census + 8, c2[5]);
+        atomicAdd(A.census + 9, c2[6]);
       }
     }
     if constexpr (!WT) {
