@@ -37,7 +37,7 @@ EXPORTS = (
     'tpe_lpdf', 'tpe_score', 'tpe_sample', 'tpe_plan_create', 'tpe_plan_destroy',
     'tpe_plan_num_levels', 'tpe_plan_set_history', 'tpe_plan_fit', 'tpe_plan_get_mixture',
     'tpe_plan_get_table',
-    'tpe_plan_suggest', 'tpe_plan_merge', 'tpe_plan_score_candidates', 'tpe_plan_last_stats',
+    'tpe_plan_suggest', 'tpe_plan_suggest_shard', 'tpe_plan_merge', 'tpe_plan_score_candidates', 'tpe_plan_last_stats',
     'tpe_plan_profile', 'tpe_plan_profile_read', 'tpe_microbench', 'tpe_plan_get_results',
     'tpe_plan_results_device', 'tpe_plan_census', 'tpe_plan_fit_suggest',
     'tpe_plan_set_lattice', 'tpe_plan_update_history', 'tpe_plan_set_prune',
@@ -140,6 +140,8 @@ def load_library(path: str = LIB_PATH):
             'tpe_plan_get_mixture': (C.c_int, [vp, i32, i32, _D, _D, _D, i64, C.POINTER(i64)]),
             'tpe_plan_get_table': (C.c_int, [vp, i32, i32, i32, vp, i64, C.POINTER(i64)]),
             'tpe_plan_suggest': (C.c_int, [vp, C.POINTER(u64), i64, i64, i64, i32, vp, i32, vp]),
+            'tpe_plan_suggest_shard': (C.c_int, [vp, C.POINTER(u64), i64, i64, i64, i64, i32, vp,
+                                                 i32, vp]),
             'tpe_plan_fit_suggest': (C.c_int, [vp, dbl, i32, dbl, i32, C.POINTER(u64), i64, i64,
                                                vp, i32, vp]),
             'tpe_plan_merge': (C.c_int, [vp, vp, i32, i32, vp, i32, vp]),
@@ -433,19 +435,24 @@ class Plan(object):
                                              buf.ctypes.data, buf.size, C.byref(n)))
         return buf
 
-    def suggest(self, seeds, n_cand, cand_begin=0, level=-1, out=None, stream=None, fetch=True):
+    def suggest(self, seeds, n_cand, cand_begin=0, level=-1, out=None, stream=None, fetch=True,
+                n_total=None):
         """Returns a structured array [n_suggest, n_hp] of RESULT_DTYPE (host)
         unless ``out`` is a device pointer (int) or ``fetch`` is False (the
-        results stay in the plan: ``results_device_ptr()`` / ``results()``)."""
+        results stay in the plan: ``results_device_ptr()`` / ``results()``).
+        ``n_total``: the candidate count of the whole suggestion when this
+        call is a shard [cand_begin, cand_begin + n_cand) of it
+        (tpe_plan_suggest_shard; default cand_begin + n_cand)."""
         e = self.engine
         seeds = _seeds(seeds)
         host = out is None and fetch
         res = np.empty((seeds.size, self.n_hp), dtype=RESULT_DTYPE) if host else None
         optr = res.ctypes.data if host else out
+        total = int(cand_begin) + int(n_cand) if n_total is None else int(n_total)
         with e.lock:
-            e.check(e.lib.tpe_plan_suggest(self.p, seeds.ctypes.data_as(C.POINTER(C.c_uint64)),
-                                           seeds.size, int(n_cand), int(cand_begin), int(level),
-                                           optr, 0 if host else 1, stream))
+            e.check(e.lib.tpe_plan_suggest_shard(
+                self.p, seeds.ctypes.data_as(C.POINTER(C.c_uint64)), seeds.size, total,
+                int(cand_begin), int(n_cand), int(level), optr, 0 if host else 1, stream))
         self._last_nsug = seeds.size
         self._last_ncand = int(n_cand)
         return res

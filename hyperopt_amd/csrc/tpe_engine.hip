@@ -436,7 +436,7 @@ int32_t set_score_groups(ScoreArgs &a, const int *kinds, int n_slots, int64_t cn
     switch (kind) {
       case KIND_ERF_G: case KIND_ERF_L: return 0;
       case KIND_LSE_G: case KIND_LSE_L: case KIND_LSE_G1: case KIND_LSE_L1:
-      case KIND_LSE_GW: case KIND_LSE_LW: return 1;
+      case KIND_LSE_GW: case KIND_LSE_LW: case KIND_LSE_GW1: case KIND_LSE_LW1: return 1;
       case KIND_LAT: return 2;
       default: return 3;
     }
@@ -595,7 +595,9 @@ int score_launch(tpe_engine *h, tpe_plan *p, ScoreArgs a, bool has_erf, int64_t 
     if (pr->n >= p->prof_cap) pr = nullptr;  // ring full: stop recording
   }
   if (pr) CKH(hipEventRecord(pr->a[pr->n], sg));
-  CKH(launch_score(a, has_erf, sg));
+  // (a level mixing wave-tile log-sum-exp slots with other kinds: those run
+  // beside it on an auxiliary stream; the events are free at scoring time)
+  CKH(launch_score(a, has_erf, sg, h->aux[1], p->ev_join[1], p->ev_join[2]));
   if (pr) {
     CKH(hipEventRecord(pr->b[pr->n], sg));
     pr->pairs[pr->n] = (double)cn * (double)a.n_suggest;
@@ -607,8 +609,11 @@ int score_launch(tpe_engine *h, tpe_plan *p, ScoreArgs a, bool has_erf, int64_t 
 // One level of conditional hps: one draw(+bucket) launch and one scoring
 // launch (every lpdf kind) for all of its hps.  Candidates are processed in
 // chunks so the buffer stays <= 2 GB (chunk_budget).
+// n_total: the candidates of the whole suggestion this call scores [cand_begin,
+// cand_begin + n_cand) of (a shard's is the unsharded count): it picks the
+// wave-tile shape, so every shard and batch of one suggestion takes the same
 int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_cand,
-              int64_t cand_begin, hipStream_t st) {
+              int64_t cand_begin, int64_t n_total, hipStream_t st) {
   const int32_t n_level = (int32_t)p->levels[level].size();
   const int32_t *lvl = p->d_level_hps + p->level_off[level];
   if (n_cand == 0) {
@@ -764,9 +769,14 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
       // tiles below 2^18 candidates measured 0.265 ms with the one-exponent
       // form -- a wave's guard sees 1/8 of the components and 3e7 pairs per
       // launch were retried -- and 0.236 ms without it, against 0.234 ms here.)
-      for (int &k : ck)
-        k = (k == KIND_LSE_G || k == KIND_LSE_G1) ? KIND_LSE_GW
-          : (k == KIND_LSE_L || k == KIND_LSE_L1) ? KIND_LSE_LW : k;
+      // (suggestions of <= kWaveRowSplitMax candidates: one-row wave tiles,
+      // 64 candidates per wave -- the dense windows' waves carry half the
+      // pairs; a small level leaves the GPU room for twice the waves)
+      for (int &k : ck) {
+        const bool one = n_total <= kWaveRowSplitMax;
+        k = (k == KIND_LSE_G || k == KIND_LSE_G1) ? (one ? KIND_LSE_GW1 : KIND_LSE_GW)
+          : (k == KIND_LSE_L || k == KIND_LSE_L1) ? (one ? KIND_LSE_LW1 : KIND_LSE_LW) : k;
+      }
     else if (small_sort)
       // one-row tiles whatever the batch size: the pruned sums depend on the
       // tile's candidate window, so a batched suggestion stays bit-identical
@@ -1343,9 +1353,17 @@ int tpe_plan_get_table(tpe_plan_t p, int32_t hp, int32_t side, int32_t which, vo
 int tpe_plan_suggest(tpe_plan_t p, const uint64_t *seeds, int64_t n_sug, int64_t n_cand,
                      int64_t cand_begin, int32_t level, tpe_result *out, int32_t out_on_device,
                      void *stream) {
+  return tpe_plan_suggest_shard(p, seeds, n_sug, cand_begin + n_cand, cand_begin, n_cand, level,
+                                out, out_on_device, stream);
+}
+
+int tpe_plan_suggest_shard(tpe_plan_t p, const uint64_t *seeds, int64_t n_sug, int64_t n_total,
+                           int64_t cand_begin, int64_t n_cand, int32_t level, tpe_result *out,
+                           int32_t out_on_device, void *stream) {
   if (!p) return TPE_E_INVALID;
   tpe_engine *h = p->eng;
-  if (n_sug <= 0 || n_cand < 0 || cand_begin < 0 || !seeds) return fail(h, TPE_E_INVALID, "bad args");
+  if (n_sug <= 0 || n_cand < 0 || cand_begin < 0 || !seeds || n_total < cand_begin + n_cand)
+    return fail(h, TPE_E_INVALID, "bad args");
   if (level >= (int32_t)p->levels.size()) return fail(h, TPE_E_INVALID, "bad level");
   CKH(hipSetDevice(h->device));
   hipStream_t st = pick_stream(h, stream);
@@ -1358,7 +1376,7 @@ int tpe_plan_suggest(tpe_plan_t p, const uint64_t *seeds, int64_t n_sug, int64_t
   const int l0 = level < 0 ? 0 : level;
   const int l1 = level < 0 ? (int)p->levels.size() : level + 1;
   for (int l = l0; l < l1; ++l) {
-    rc = run_level(h, p, l, n_sug, n_cand, cand_begin, st);
+    rc = run_level(h, p, l, n_sug, n_cand, cand_begin, n_total, st);
     if (rc) return rc;
   }
   if (p->prof_cap > 0) CKH(hipEventRecord(p->ev1, st));
@@ -1379,7 +1397,7 @@ int enqueue_step(tpe_engine *h, tpe_plan *p, int32_t nb, double prior_weight, in
   CKH(launch_fit(fit_args(p, nb, prior_weight, lf), p->P, st));
   p->last_nb = nb;
   for (int l = 0; l < (int)p->levels.size(); ++l) {
-    const int rc = run_level(h, p, l, n_sug, n_cand, 0, st);
+    const int rc = run_level(h, p, l, n_sug, n_cand, 0, n_cand, st);
     if (rc) return rc;
   }
   return TPE_OK;
@@ -1747,7 +1765,7 @@ static bool small_sort_on() {
 static bool moment_on() {
   static const bool v = [] {
     const char *e = std::getenv("TPE_MOMENT");
-    return e && std::atoi(e) != 0;  // (off until verified on the GPU)
+    return !(e && std::atoi(e) == 0);
   }();
   return v;
 }

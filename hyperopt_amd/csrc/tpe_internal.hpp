@@ -24,15 +24,28 @@ constexpr int kMaxLeaves = 160;  // numpy pairwise leaves per 8192 chunk (<=128)
 // candidates with the block skip and the wave-wide exponent: every wave owns
 // its own 128 candidates and all of both mixtures' live components (no
 // cross-wave partials); a block is 8 such wave tiles
+// KIND_LSE_GW1 / KIND_LSE_LW1: the same wave tiles with one candidate row
+// (64 candidates per wave): for suggestions of at most kWaveRowSplitMax
+// candidates, whose levels are too small to fill the GPU -- the waves of
+// dense value windows (most live component blocks) then carry half the pairs
+// and end the launch sooner (run_level, chosen by the per-suggestion
+// candidate count, so a batch and every shard take the same tiles)
 enum { KIND_LSE_G = 0, KIND_LSE_L = 1, KIND_ERF_G = 2, KIND_ERF_L = 3, KIND_CAT = 4,
-       KIND_LAT = 5, KIND_LSE_G1 = 6, KIND_LSE_L1 = 7, KIND_LSE_GW = 8, KIND_LSE_LW = 9 };
+       KIND_LAT = 5, KIND_LSE_G1 = 6, KIND_LSE_L1 = 7, KIND_LSE_GW = 8, KIND_LSE_LW = 9,
+       KIND_LSE_GW1 = 10, KIND_LSE_LW1 = 11 };
+constexpr int64_t kWaveRowSplitMax = (int64_t)1 << 18;
 
 __host__ __device__ constexpr bool kind_lse(int k) {
   return k == KIND_LSE_G || k == KIND_LSE_L || k == KIND_LSE_G1 || k == KIND_LSE_L1 ||
-         k == KIND_LSE_GW || k == KIND_LSE_LW;
+         k == KIND_LSE_GW || k == KIND_LSE_LW || k == KIND_LSE_GW1 || k == KIND_LSE_LW1;
 }
 __host__ __device__ constexpr bool kind_logn(int k) {
-  return k == KIND_LSE_L || k == KIND_LSE_L1 || k == KIND_LSE_LW || k == KIND_ERF_L;
+  return k == KIND_LSE_L || k == KIND_LSE_L1 || k == KIND_LSE_LW || k == KIND_LSE_LW1 ||
+         k == KIND_ERF_L;
+}
+// wave-tile log-sum-exp kinds (value-bucketed candidates, block skip)
+__host__ __device__ constexpr bool kind_wave_lse(int k) {
+  return k == KIND_LSE_GW || k == KIND_LSE_LW || k == KIND_LSE_GW1 || k == KIND_LSE_LW1;
 }
 
 __host__ __device__ inline int score_kind(const tpe_hp &h) {
@@ -44,7 +57,8 @@ __host__ __device__ inline int score_kind(const tpe_hp &h) {
 
 // candidate rows (per lane) of a scoring tile of the kind: 64 * rows candidates
 __host__ __device__ constexpr int tile_rows(int kind) {
-  return (kind == KIND_ERF_G || kind == KIND_ERF_L || kind == KIND_LSE_G1 || kind == KIND_LSE_L1)
+  return (kind == KIND_ERF_G || kind == KIND_ERF_L || kind == KIND_LSE_G1 || kind == KIND_LSE_L1 ||
+          kind == KIND_LSE_GW1 || kind == KIND_LSE_LW1)
              ? 1
          : (kind == KIND_CAT || kind == KIND_LAT) ? 4 : 2;
 }
@@ -54,8 +68,7 @@ __host__ __device__ constexpr int tile_rows(int kind) {
 // takes its own 256 candidates (one-wave tiles left 7 of 8 waves idle, and
 // a 1e6-candidate slot 3906 blocks instead of 489).
 __host__ __device__ constexpr int tile_waves(int kind) {
-  return (kind == KIND_LSE_GW || kind == KIND_LSE_LW || kind == KIND_CAT || kind == KIND_LAT) ? 8
-                                                                                             : 1;
+  return (kind_wave_lse(kind) || kind == KIND_CAT || kind == KIND_LAT) ? 8 : 1;
 }
 // candidates of one scoring block of the kind
 __host__ __device__ constexpr int tile_cands(int kind) {
@@ -298,7 +311,12 @@ hipError_t launch_prep(const tpe_hp *hps, int32_t n_hp, const double *mw,
                        const double *mmu, const double *msig, MixInfo *info,
                        Coef *coef, Coef32 *coef32, CoefM *coefm, int64_t kcap, double *scratch,
                        hipStream_t st);
-hipError_t launch_score(const ScoreArgs &a, bool has_erf, hipStream_t st);
+// a level mixing wave-tile log-sum-exp groups with other kinds runs two
+// launches: the other kinds on `side` between fork / join events (when side
+// is given; st waits for the join), the log-sum-exp groups on st
+hipError_t launch_score(const ScoreArgs &a, bool has_erf, hipStream_t st,
+                        hipStream_t side = nullptr, hipEvent_t ev_fork = nullptr,
+                        hipEvent_t ev_join = nullptr);
 // lpdf pairs of every lattice point of the first n_lat hps of a level
 // (hps_of_level[], host arrays; one block of kLatThreads per point, up to
 // kLatJobs hps per launch), written to lat_out

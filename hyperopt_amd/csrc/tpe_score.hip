@@ -629,10 +629,10 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
         // sigmas equal and x = |v| xh <= kMomXLim over the wave's whole
         // candidate range -- and the chunk is taken when either of its two
         // blocks is live; its blocks then leave the pair and wide loops
-        static_assert(KR == 2, "the moment form packs the lane's two candidate rows");
+        // (the moment form packs the lane's two candidate rows: two-row tiles only)
         constexpr uint64_t kEven = 0x5555555555555555ull;
         bool elig = false;
-        if (cmv && has && !(lane & 1)) {
+        if (KR == 2 && cmv && has && !(lane & 1)) {
           const CoefM *q = cmv + (r0 + (lane >> 1));
           const float cf = (float)q->center;
           const float x = fmaxf(fabsf(win.lo - cf), fabsf(win.hi - cf)) * q->xh;
@@ -654,7 +654,7 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
           cen.exec += lx * (uint32_t)nvalid;
           cen.shift += lx * (uint32_t)nvalid;
         }
-        {
+        if constexpr (KR == 2) {
           KCM *rm = uniform_ptrm(cmv) + r0;
           uint64_t cm = cmask;
           bool hm = cm != 0;
@@ -1064,9 +1064,25 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
   int64_t li[KR];
   bool valid[KR];
   double x[KR], y[KR], ub[KR], lb[KR];
+  // the wave's 64 * KR candidates.  Log-sum-exp wave tiles: the block's 8
+  // waves take wave tiles spread over their 4096-candidate sort block (wave
+  // w of the q-th of the sort block's nbs blocks: wave tile q + nbs w), not 8
+  // consecutive ones -- a sort block spans the whole value range bucket by
+  // bucket, so its dense value windows (the waves with the most live
+  // component blocks) are shared out over blocks, CUs and SIMDs instead of
+  // landing on one CU together.  A wave's sums depend only on its own
+  // candidates: the mapping changes no result.
+  int64_t wt0 = (int64_t)tile * tile_cands(KIND) + (WT ? wave * 64 * KR : 0);
+  if constexpr (kind_wave_lse(KIND)) {
+    constexpr int SBB = kSortedBlock / tile_cands(KIND);  // blocks per sort block
+    static_assert(SBB * tile_cands(KIND) == kSortedBlock, "blocks tile the sort block");
+    const int sb = tile / SBB, q = tile % SBB;
+    const int nbs = min(SBB, ntiles - sb * SBB);
+    wt0 = ((int64_t)sb * SBB * kWaves + q + (int64_t)nbs * wave) * 64 * KR;
+  }
 #pragma unroll
   for (int r = 0; r < KR; ++r) {
-    li[r] = (int64_t)tile * tile_cands(KIND) + (WT ? wave * 64 * KR : 0) + r * 64 + lane;
+    li[r] = wt0 + r * 64 + lane;
     valid[r] = li[r] < A.n_cand;
     x[r] = valid[r] ? cand[li[r]] : (LOGN ? 1.0 : 0.0);
     y[r] = ub[r] = lb[r] = 0.0;
@@ -1561,7 +1577,7 @@ __device__ __forceinline__ void mark_inactive(const ScoreArgs &A, int s, int s0,
 // erf ones, every kind, or only the wave-tile log-sum-exp kinds (levels of
 // large draws whose every slot is one: a kernel with only their register
 // allocation -- the combined one keeps the most any kind needs).
-enum { kSetNoErf = 0, kSetAll = 1, kSetWave = 2 };
+enum { kSetNoErf = 0, kSetAll = 1, kSetWave = 2, kSetWave1 = 3 };
 
 template <int SET, bool CENSUS>
 __device__ __forceinline__ void score_block(const ScoreArgs &A, ScoreSmem &sm) {
@@ -1583,6 +1599,10 @@ __device__ __forceinline__ void score_block(const ScoreArgs &A, ScoreSmem &sm) {
   if constexpr (SET == kSetWave) {
     if (A.grp_kind[g] == KIND_LSE_LW) score_tile<KIND_LSE_LW, CENSUS>(A, sm, slot, tile, nt, known);
     else score_tile<KIND_LSE_GW, CENSUS>(A, sm, slot, tile, nt, known);
+    return;
+  } else if constexpr (SET == kSetWave1) {
+    if (A.grp_kind[g] == KIND_LSE_LW1) score_tile<KIND_LSE_LW1, CENSUS>(A, sm, slot, tile, nt, known);
+    else score_tile<KIND_LSE_GW1, CENSUS>(A, sm, slot, tile, nt, known);
     return;
   } else {
     switch (A.grp_kind[g]) {
@@ -1619,6 +1639,14 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(TPE
 void k_score_wave(ScoreArgs A) {
   __shared__ ScoreSmem sm;
   score_block<kSetWave, CENSUS>(A, sm);
+}
+// the one-row wave tiles (KIND_LSE_GW1 / LW1) in a kernel of their own: the
+// two-row kernel's register allocation is left as it is
+template <bool CENSUS>
+__global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(TPE_WAVE_EU)))
+void k_score_wave1(ScoreArgs A) {
+  __shared__ ScoreSmem sm;
+  score_block<kSetWave1, CENSUS>(A, sm);
 }
 
 // Value-lattice scoring of the bounded quantized hps (KIND_LAT).  A drawn
@@ -1827,15 +1855,59 @@ hipError_t launch_lattice_draw(const ScoreArgs &a, const int32_t *hps_of_level, 
   return hipGetLastError();
 }
 
-hipError_t launch_score(const ScoreArgs &a, bool has_erf, hipStream_t st) {
+// the groups of a (kind) subset of a launch's grid, renumbered
+static ScoreArgs select_groups(const ScoreArgs &a, bool wave_lse) {
+  ScoreArgs b = a;
+  b.n_groups = 0;
+  int32_t blocks = 0;
+  for (int i = 0; i < a.n_groups; ++i) {
+    if (kind_wave_lse(a.grp_kind[i]) != wave_lse) continue;
+    const int j = b.n_groups++;
+    b.grp_kind[j] = a.grp_kind[i];
+    b.grp_slot0[j] = a.grp_slot0[i];
+    b.grp_tiles[j] = a.grp_tiles[i];
+    b.grp_slots[j] = a.grp_slots[i];
+    b.grp_block0[j] = blocks;
+    blocks += a.grp_block0[i + 1] - a.grp_block0[i];
+  }
+  b.grp_block0[b.n_groups] = blocks;
+  return b;
+}
+
+hipError_t launch_score(const ScoreArgs &a, bool has_erf, hipStream_t st, hipStream_t side,
+                        hipEvent_t ev_fork, hipEvent_t ev_join) {
   if (a.n_groups <= 0 || a.n_suggest <= 0) return hipSuccess;
   const int blocks = a.grp_block0[a.n_groups];
   if (blocks <= 0) return hipSuccess;
+  bool any_wave = false, all_wave = true, one_row = false;
+  for (int i = 0; i < a.n_groups; ++i) {
+    const bool w = kind_wave_lse(a.grp_kind[i]);
+    any_wave |= w;
+    all_wave &= w;
+    one_row |= a.grp_kind[i] == KIND_LSE_GW1 || a.grp_kind[i] == KIND_LSE_LW1;
+  }
+  if (any_wave && !all_wave) {
+    // a level of wave-tile log-sum-exp slots and other kinds (lookups,
+    // quantized): the log-sum-exp groups run their own wave kernel, the rest
+    // the combined one -- beside it on the side stream when one is given
+    const ScoreArgs w = select_groups(a, true), o = select_groups(a, false);
+    hipError_t e;
+    if (side) {
+      if ((e = hipEventRecord(ev_fork, st)) != hipSuccess) return e;
+      if ((e = hipStreamWaitEvent(side, ev_fork, 0)) != hipSuccess) return e;
+    }
+    const hipError_t eo = launch_score(o, has_erf, side ? side : st, nullptr, nullptr, nullptr);
+    // (once forked, the side stream is joined back on every path)
+    const hipError_t ej = side ? hipEventRecord(ev_join, side) : hipSuccess;
+    const hipError_t ew = launch_score(w, false, st, nullptr, nullptr, nullptr);
+    if (side && ej == hipSuccess && (e = hipStreamWaitEvent(st, ev_join, 0)) != hipSuccess) return e;
+    return eo != hipSuccess ? eo : ej != hipSuccess ? ej : ew;
+  }
   const dim3 g((unsigned)blocks, a.n_suggest);
-  bool wave_only = true;
-  for (int i = 0; i < a.n_groups; ++i)
-    wave_only &= a.grp_kind[i] == KIND_LSE_GW || a.grp_kind[i] == KIND_LSE_LW;
-  if (wave_only) {
+  if (all_wave && one_row) {
+    if (a.census) k_score_wave1<true><<<g, kWaves * 64, 0, st>>>(a);
+    else k_score_wave1<false><<<g, kWaves * 64, 0, st>>>(a);
+  } else if (all_wave) {
     if (a.census) k_score_wave<true><<<g, kWaves * 64, 0, st>>>(a);
     else k_score_wave<false><<<g, kWaves * 64, 0, st>>>(a);
   } else if (has_erf) {

@@ -156,7 +156,7 @@ class ShardedSuggest(object):
             local = torch.empty(S * P * RECORD_BYTES, dtype=torch.uint8, device=self.device)
             for level in range(self.plan.n_levels):
                 self.plan.suggest(seeds, count, cand_begin=begin, level=level,
-                                  out=local.data_ptr(), stream=stream)
+                                  out=local.data_ptr(), stream=stream, n_total=int(n_cand))
                 gathered = self.gather(local)
                 self.plan.merge(gathered.data_ptr(), self.world, level, out=local.data_ptr(),
                                 stream=stream, n_suggest=S)

@@ -207,6 +207,15 @@ int tpe_plan_get_table(tpe_plan_t p, int32_t hp, int32_t side, int32_t which, vo
 int tpe_plan_suggest(tpe_plan_t p, const uint64_t *seeds, int64_t n_suggest,
                      int64_t n_cand, int64_t cand_begin, int32_t level,
                      tpe_result *out, int32_t out_on_device, void *stream);
+/* The same for a shard of a larger suggestion: the candidates [cand_begin,
+ * cand_begin + n_cand) of an n_total-candidate suggestion (n_total >=
+ * cand_begin + n_cand).  n_total picks the scoring tiles (one-row wave tiles
+ * up to 2^18 candidates), so the shards of one suggestion score every
+ * candidate exactly as the unsharded call does (parallel.ShardedSuggest);
+ * tpe_plan_suggest is this with n_total = cand_begin + n_cand.             */
+int tpe_plan_suggest_shard(tpe_plan_t p, const uint64_t *seeds, int64_t n_sug, int64_t n_total,
+                           int64_t cand_begin, int64_t n_cand, int32_t level, tpe_result *out,
+                           int32_t out_on_device, void *stream);
 
 /* tpe_plan_fit + tpe_plan_suggest (all levels, cand_begin 0) in one call:
  * the tpe.suggest posterior evaluation for one history.  Repeated calls of
