@@ -177,6 +177,8 @@ static_assert(sizeof(Coef32) == 128, "two 64-B scalar loads");
 constexpr int kMomChunk = 16;
 constexpr int kMomDeg = 9;
 constexpr float kMomXLim = 0.65f;
+constexpr float kMomXCap = 2.5f;          // beyond: never (the Horner sum's conditioning)
+constexpr float kMomLog2Fact = 21.79106f; // log2((kMomDeg + 1)!) = log2(10!)
 struct __attribute__((aligned(64))) CoefM {
   double center;   // mu' midpoint of the chunk (fp64)
   float base;      // integer near T* (A - M is exact)

@@ -590,9 +590,11 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
       const int k0 = round_k<STRIDE>(r0, lane);
       const bool has = r0 + STRIDE * (lane >> 1) < nch && k0 < nb;
       bool live = false, wide = false;
+      float bnd = -INFINITY;  // the block's envelope bound over the window
       if (has) {
         const float4 e = *reinterpret_cast<const float4 *>(tb + coef_off(k0, 3));
-        live = envelope_bound(e, win) >= win.thr;
+        bnd = envelope_bound(e, win);
+        live = bnd >= win.thr;
         wide = __builtin_signbit(e.w);
       }
       if constexpr (CENSUS) {
@@ -631,12 +633,24 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
         // blocks is live; its blocks then leave the pair and wide loops
         // (the moment form packs the lane's two candidate rows: two-row tiles only)
         constexpr uint64_t kEven = 0x5555555555555555ull;
+        // Eligibility: the truncation bound tau(x) = x^(D+1) / (D+1)! e^x (D =
+        // kMomDeg) relative to the chunk's terms, which are at most 2^bound
+        // (the larger of its two blocks' envelope bounds) against the lane's
+        // largest term >= 2^L, L = thr + dead + 1 (lse_window): taken when x
+        // <= kMomXLim (tau <= 7.1e-9 whatever the chunk weighs) or when
+        // log2 tau + bound <= thr + 1, i.e. tau 2^(bound - L) <= 2^-dead, the
+        // skipped blocks' budget per component -- far chunks of a wide halo
+        // qualify at larger x -- and x <= kMomXCap (fp32 Horner conditioning
+        // e^(2x) bounded)
+        const float bnd1 = __builtin_bit_cast(float, dpp<kDppXor1>(__builtin_bit_cast(int, bnd)));
         bool elig = false;
         if (KR == 2 && cmv && has && !(lane & 1)) {
           const CoefM *q = cmv + (r0 + (lane >> 1));
           const float cf = (float)q->center;
           const float x = fmaxf(fabsf(win.lo - cf), fabsf(win.hi - cf)) * q->xh;
-          elig = x <= kMomXLim;
+          const float l2tau = (float)(kMomDeg + 1) * __builtin_amdgcn_logf(x) +
+                              x * 1.44269504f - kMomLog2Fact;
+          elig = x <= kMomXLim || (x <= kMomXCap && l2tau + fmaxf(bnd, bnd1) <= win.thr + 1.0f);
         }
         const uint64_t lm = __ballot(live);
         const uint64_t cmask = (lm | (lm >> 1)) & __ballot(elig) & kEven;
@@ -979,9 +993,16 @@ __device__ __forceinline__ void erf_chunks(KDbl *__restrict__ cs, int c0, int nb
 // clock (100 MHz) at entry, after the component loop and at the end, plus the
 // (slot, tile) and hardware ids of the block, for the blocks of suggestion 0
 __device__ unsigned long long g_score_stamps[8192][4];
+// (TPE_STAMPS_WAVE_LSE: only the wave-tile log-sum-exp launches stamp -- a
+// mixed level's lookup launch runs beside it and would overwrite its rows)
+#ifdef TPE_STAMPS_WAVE_LSE
+#define STAMP_KIND_OK kind_wave_lse(KIND)
+#else
+#define STAMP_KIND_OK true
+#endif
 #define SSTAMP(i)                                                                        \
   do {                                                                                   \
-    if (threadIdx.x == 0 && blockIdx.y == 0) {                                           \
+    if (STAMP_KIND_OK && threadIdx.x == 0 && blockIdx.y == 0) {                          \
       const unsigned b = blockIdx.x & 8191;                                              \
       g_score_stamps[b][i] = wall_clock64();                                             \
       if (i == 0)                                                                        \
@@ -992,8 +1013,17 @@ __device__ unsigned long long g_score_stamps[8192][4];
             (__builtin_amdgcn_s_getreg(63488 | 4) & 0xffff);                             \
     }                                                                                    \
   } while (0)
+// per wave (wave tiles): start and end of the component loops, lane 0 of
+// every wave of the blocks of suggestion 0
+__device__ unsigned long long g_wave_stamps[8192][kWaves][2];
+#define WSTAMP(i)                                                                        \
+  do {                                                                                   \
+    if ((threadIdx.x & 63) == 0 && blockIdx.y == 0)                                      \
+      g_wave_stamps[blockIdx.x & 8191][threadIdx.x >> 6][i] = wall_clock64();            \
+  } while (0)
 #else
 #define SSTAMP(i) do {} while (0)
+#define WSTAMP(i) do {} while (0)
 #endif
 
 struct ScoreSmem {
@@ -1049,6 +1079,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
   if constexpr (WT) {  // the block's arrival counter (finalize), before any wave can arrive
     if (threadIdx.x == 0) sm.arrive = 0u;
     __syncthreads();
+    WSTAMP(0);
   }
   const int64_t sb = 2 * (int64_t)hp, sa = sb + 1;
   const MixInfo ib = A.info[sb], ia = A.info[sa];
@@ -1267,6 +1298,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
     }
   }
   SSTAMP(1);
+  if constexpr (WT) WSTAMP(1);
   if (!WT && wave != 0) return;
 
   // ---- finalize (every wave of a wave tile, wave 0 of an 8-wave tile):
@@ -1532,6 +1564,10 @@ namespace tpe {
 }  // namespace tpe
 extern "C" int tpe_debug_score_stamps(unsigned long long *out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(tpe::g_score_stamps), sizeof(tpe::g_score_stamps)) ==
+                 hipSuccess ? 0 : -5;
+}
+extern "C" int tpe_debug_wave_stamps(unsigned long long *out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(tpe::g_wave_stamps), sizeof(tpe::g_wave_stamps)) ==
                  hipSuccess ? 0 : -5;
 }
 namespace tpe {

@@ -137,7 +137,7 @@ def test_config4_reference_candidates_production_form(cfg4_plan):
             assert_close(la, ra, msg='cfg4 %s above, mode %d' % (lab, mode))
             assert argmax_equiv(rb - ra, bi), (lab, mode)
             stats[lab] = dict(below=_delta(lb, rb), above=_delta(la, ra))
-        census = plan.census(False)
+        census = plan.census(False, n=10)
         total, shifted, evaluated = census[3], census[4], census[5]
         # (a wave whose one-exponent guard fails counts its pairs again in
         # the exact loop it falls back to)
@@ -149,6 +149,13 @@ def test_config4_reference_candidates_production_form(cfg4_plan):
             assert shifted > 0.9 * evaluated, census     # the one-exponent form ran
         else:
             assert shifted == 0
+        # the moment form of equal-sigma chunks (CoefM): mode 3 only, most of
+        # the config-4 pairs (sigmas at the prior_sigma / 100 floor), unless
+        # TPE_MOMENT=0 (test_moment_env_off)
+        if mode == 3 and os.environ.get('TPE_MOMENT', '1') != '0':
+            assert census[9] > 0.5 * evaluated, census
+        else:
+            assert census[9] == 0, census
         _record('cfg4_reference_candidates_mode%d' % mode, census=list(census), **stats)
 
 
@@ -499,6 +506,16 @@ def test_shift_min_env_exact_loop():
     assert '1 passed' in out, out[-2000:]
 
 
+def test_moment_env_off():
+    """TPE_MOMENT=0 (the moment form of equal-sigma chunks off: every
+    one-exponent pair in the block-local fp32 pair form): the config-4
+    reference-candidate parity test in a child process with that switch."""
+    out = _child('import sys, pytest; sys.exit(pytest.main(["-q", "-x", "-m", "gpu", '
+                 '"tests/test_gpu_shifted.py::test_config4_reference_candidates_production_form"]))',
+                 {'TPE_MOMENT': '0'})
+    assert '1 passed' in out, out[-2000:]
+
+
 def test_chunk_budget_env_identical_results():
     """TPE_CHUNK_MB (candidate buffer per scoring chunk): a 64 MB budget runs
     a 1e6-candidate config-2 suggest in 3 chunks (accumulated winners), the
@@ -552,3 +569,53 @@ def test_sorted_wave_tiles_argmax_numpy_semantics():
         with np.errstate(invalid='ignore'):
             assert bi == int(np.argmax(lb - la)) == 77_777, (lab, bi)
         assert np.isnan(bs)
+
+
+_MOM = np.dtype([('center', '<f8'), ('base', '<f4'), ('cm', '<f4'), ('gam', '<f4'),
+                 ('m', '<f4', (10,)), ('xh', '<f4')])
+
+
+def test_moment_table_vs_numpy(cfg4_plan):
+    """The fit's moment table (CoefM, tpe_plan_get_table) of config-4
+    mixtures against a float64 numpy restatement from the plan's own fitted
+    mixture: per 16-component chunk of mu-sorted components, centre = mu'
+    midpoint, T_k = c_k - a^2 d_k^2, T* = max, m_j = sum_k 2^(T_k - T*) q_k^j / j!
+    with q_k = 2 a^2 ln2 d_k, xh = max |q_k|; chunks whose sigmas differ (the
+    prior's) are not eligible (xh = +inf).  fp32 fields to fp32 rounding."""
+    dom, plan = cfg4_plan
+    LOG2E, LN2 = 1.4426950408889634, math.log(2.0)
+    for lab in ('x0', 'x57'):
+        hp_i = dom.space.by_label[lab].index
+        for side in (0, 1):
+            w, mu, sg = plan.mixture(hp_i, side)
+            t = plan.table(hp_i, side, 2).view(_MOM)
+            K = w.size
+            sgc = np.maximum(sg, 1e-12)
+            from oracle import tpe_oracle as O
+            pacc = np.sum(w * (O.normal_cdf(5.0, mu, sgc) - O.normal_cdf(-5.0, mu, sgc)))
+            c = LOG2E * np.log(w / np.sqrt(2 * np.pi * sgc ** 2) / pacc)
+            a2 = LOG2E / (2 * sgc ** 2)
+            n_ok = 0
+            for ch in range(-(-K // 16)):
+                sl = slice(16 * ch, min(K, 16 * ch + 16))
+                m_, a2_, c_ = mu[sl], a2[sl], c[sl]
+                e = t[ch]
+                if not np.all(a2_ == a2_[0]):
+                    assert np.isinf(e['xh']), (lab, side, ch)
+                    continue
+                n_ok += 1
+                cen = 0.5 * (m_.min() + m_.max())
+                d = m_ - cen
+                T = c_ - a2_ * d * d
+                Ts = T.max()
+                rho = np.exp2(T - Ts)
+                q = 2 * a2_[0] * LN2 * d
+                mom = np.array([np.sum(rho * q ** j) / math.factorial(j) for j in range(10)])
+                assert e['center'] == cen
+                np.testing.assert_allclose(e['xh'], np.abs(q).max(), rtol=2e-7)   # (rounded up)
+                assert e['base'] == np.floor(Ts)
+                np.testing.assert_allclose(e['cm'], Ts - np.floor(Ts), atol=2e-7)
+                np.testing.assert_allclose(e['gam'], -a2_[0], rtol=1e-7)
+                np.testing.assert_allclose(e['m'], mom, rtol=2e-7, atol=1e-30)
+            if side == 1:
+                assert n_ok >= 0.99 * (-(-K // 16)) - 1, (lab, n_ok)

@@ -42,6 +42,7 @@ LOG2E = 1.4426950408889634
 LN2 = math.log(2.0)
 P = 9           # degree (10 moments), tpe_internal.hpp kMomDeg
 X_LIM = 0.65    # x^(P+1)/(P+1)! e^x <= 7.1e-9, kMomXLim
+X_CAP = 2.5     # kMomXCap
 CH = 16         # components per chunk, kMomChunk
 
 
@@ -116,8 +117,17 @@ def score(B, y):
     t = B['c'].reshape(-1)[None, :] - B['a2'].reshape(-1)[None, :] * (y[:, None] - B['m'].reshape(-1)[None, :]) ** 2
     M = np.ceil(np.max(t)) + 1.0
     lo, hi = y.min(), y.max()
-    vmax = np.maximum.reduce([np.abs(lo - B['lo']), np.abs(lo - B['hi']), np.abs(hi - B['lo']), np.abs(hi - B['hi'])])
-    use = vmax * B['xh'] <= X_LIM
+    x = np.maximum(np.abs(lo - B['cen']), np.abs(hi - B['cen'])) * B['xh']
+    # weighted criterion (tpe_score.hip): tau(x) 2^(bound - L) <= 2^-dead,
+    # bound = the chunk's largest term over the window, L = the smallest lane
+    # maximum (the kernel uses envelope bounds and the tightened threshold)
+    tt = t.reshape(y.size, nb, CH)
+    bound = tt.max(axis=(0, 2))
+    L = t.max(axis=1).min()
+    dead = 26 + math.ceil(math.log2(max(t.shape[1] - 1, 1)))
+    with np.errstate(divide='ignore'):
+        l2tau = (P + 1) * np.log2(x) + x * math.log2(math.e) - math.log2(math.factorial(P + 1))
+    use = (x <= X_LIM) | ((x <= X_CAP) & (l2tau + bound <= L - dead))
     bs = np.empty((y.size, nb), np.float32)
     # moment blocks
     v = f32(y[:, None] - B['cen'][None, :])                       # (n, nb)

@@ -63,6 +63,30 @@ def main(cfg, n_cand):
         print('%2d tiles %3d  start %6.1f..%6.1f  loop %6.1f (max %6.1f)  tail %5.1f  end max %6.1f' %
               (sl, (slot == sl).sum(), r[:, 0].min(), r[:, 0].max(), (r[:, 1] - r[:, 0]).mean(),
                (r[:, 1] - r[:, 0]).max(), (r[:, 2] - r[:, 1]).mean(), r[:, 2].max()))
+    # per wave (wave tiles): component-loop durations and the block ends
+    wb = (C.c_ulonglong * (8192 * 8 * 2))()
+    if hasattr(eng.lib, 'tpe_debug_wave_stamps') and eng.lib.tpe_debug_wave_stamps(wb) == 0:
+        ws = np.frombuffer(wb, dtype=np.uint64).reshape(8192, 8, 2).astype(np.int64)[:nb]
+        okw = (ws[:, :, 0] > 0) & (ws[:, :, 1] >= ws[:, :, 0])
+        if okw.any():
+            t0 = t[:, 0].min()
+            dur = (ws[:, :, 1] - ws[:, :, 0]) / 100.0
+            start = (ws[:, :, 0] - t0) / 100.0
+            end = (ws[:, :, 1] - t0) / 100.0
+            d = dur[okw]
+            print('wave loops: %d waves, mean %.1f us, p50 %.1f, p90 %.1f, max %.1f; wave starts '
+                  '%.1f..%.1f, loop ends max %.1f us' % (d.size, d.mean(), np.median(d),
+                                                          np.quantile(d, 0.9), d.max(),
+                                                          start[okw].min(), start[okw].max(),
+                                                          end[okw].max()))
+            bend = np.where(okw, end, -1).max(axis=1)
+            sel = bend >= 0
+            print('block ends (last wave loop): mean %.1f us, max %.1f us (max / mean %.2f)' %
+                  (bend[sel].mean(), bend[sel].max(), bend[sel].max() / bend[sel].mean()))
+            # loop time by the wave's place in its 4096-candidate sort block
+            # (dense value windows), from the tile mapping of tpe_score.hip
+            hist = np.histogram(d, bins=[0, 2, 5, 10, 20, 40, 80, 1e9])[0]
+            print('wave loop histogram (us: 0-2,2-5,5-10,10-20,20-40,40-80,80+):', hist.tolist())
     key = xcc * 64 + se * 16 + cu
     u, c = np.unique(key, return_counts=True)
     print('distinct (xcd, se, cu) ids: %d; blocks per id min/max %d/%d; per xcd %s' %
