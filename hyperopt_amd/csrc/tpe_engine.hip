@@ -21,6 +21,13 @@ using namespace tpe;
 static int lse_shift_min();
 static bool small_sort_on();
 static int64_t chunk_budget();
+// TPE_SIDE_STREAMS=1: the lattice launch and a mixed level's lookup launch
+// run on auxiliary streams beside the draw / the wave-tile launch (fork and
+// join events); default off: every launch in order on the suggest stream
+static bool side_streams_on() {
+  static const bool on = std::getenv("TPE_SIDE_STREAMS") != nullptr;
+  return on;
+}
 static bool moment_on();
 constexpr int64_t kSmallSortMin = 2048;  // candidates per chunk worth bucketing a small draw
 
@@ -597,7 +604,8 @@ int score_launch(tpe_engine *h, tpe_plan *p, ScoreArgs a, bool has_erf, int64_t 
   if (pr) CKH(hipEventRecord(pr->a[pr->n], sg));
   // (a level mixing wave-tile log-sum-exp slots with other kinds: those run
   // beside it on an auxiliary stream; the events are free at scoring time)
-  CKH(launch_score(a, has_erf, sg, h->aux[1], p->ev_join[1], p->ev_join[2]));
+  CKH(launch_score(a, has_erf, sg, side_streams_on() ? h->aux[1] : nullptr, p->ev_join[1],
+                   p->ev_join[2]));
   if (pr) {
     CKH(hipEventRecord(pr->b[pr->n], sg));
     pr->pairs[pr->n] = (double)cn * (double)a.n_suggest;
@@ -678,11 +686,14 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
     for (int i = n_lat; i < n_level; ++i)
       erf_level |= kinds[i] == KIND_ERF_G || kinds[i] == KIND_ERF_L;
   }
-  // the lattice needs only the fitted mixtures: unless it carries the draw
-  // (fuse_draw), it runs on a side stream beside the candidate draw (fork /
-  // join events; a parallel branch of the captured graph), and the scoring
-  // launch waits for it
-  const bool lat_side = lat_level && !fuse_draw;
+  // the lattice needs only the fitted mixtures: with TPE_SIDE_STREAMS=1 (and
+  // unless it carries the draw, fuse_draw) it runs on a side stream beside the
+  // candidate draw (fork / join events; a parallel branch of the captured
+  // graph), and the scoring launch waits for it.  Default: in order on the
+  // suggest stream -- round 5, config 3: 0.193 ms per suggest in order against
+  // 0.201 ms forked (the cross-stream joins cost more than the overlap saves;
+  // configs 2 and 5 unchanged, profiles/rd5h_*)
+  const bool lat_side = lat_level && !fuse_draw && side_streams_on();
   if (lat_level && !fuse_draw) {
     ScoreArgs la = base_args(p, n_sug);
     la.level_hps = lvl;

@@ -28,6 +28,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "tpe_device.hpp"
 #include "tpe_draw.hpp"
@@ -177,9 +178,74 @@ __device__ __forceinline__ void mom_terms(const MomGroup &g, float Mf, const dou
 #pragma unroll
   for (int q = kMomDeg - 2; q >= 0; --q) p = __builtin_elementwise_fma(p, v, f2v{g.m[q], g.m[q]});
 }
+// one candidate row (one-row wave tiles): two chunks a, b packed instead of
+// two rows, the same arithmetic per (candidate, chunk)
+__device__ __forceinline__ void mom_terms2(const MomGroup &a, const MomGroup &b, float Mf, double y,
+                                           f2v &arg, f2v &p) {
+  const f2v off = {a.cm + (a.A - Mf), b.cm + (b.A - Mf)};
+  const f2v v = {(float)(y - a.c), (float)(y - b.c)};
+  arg = __builtin_elementwise_fma(f2v{a.g, b.g}, v * v, off);
+  p = __builtin_elementwise_fma(f2v{a.m[kMomDeg], b.m[kMomDeg]}, v,
+                                f2v{a.m[kMomDeg - 1], b.m[kMomDeg - 1]});
+#pragma unroll
+  for (int q = kMomDeg - 2; q >= 0; --q) p = __builtin_elementwise_fma(p, v, f2v{a.m[q], b.m[q]});
+}
 __device__ __forceinline__ void mom_sum(const f2v &arg, const f2v &p, float (&bs)[2]) {
   bs[0] = __builtin_amdgcn_exp2f(arg.x) * p.x;
   bs[1] = __builtin_amdgcn_exp2f(arg.y) * p.y;
+}
+
+// Tables staged in LDS (the one-row wave-tile kernel, k_score_wave1): a
+// mixture's block envelopes and block-local fp32 blocks copied once per
+// workgroup, so the component loops of its 8 waves read them at LDS latency
+// instead of waiting on one scalar-load batch per block (the small launches
+// that kernel serves are latency-bound, not VALU-bound).  The values are the
+// global tables' bit for bit: staging changes no result.
+#ifdef TPE_STAMPS
+// diagnostic build only (tools/score_stamps.py): per wave of suggestion 0's
+// wave tiles, [0] component blocks evaluated by the one-exponent loops, [1]
+// their attempts, [2] fallbacks to the exact loop, [3] blocks the exact loop
+// evaluated
+__device__ unsigned g_wave_info[8192][8][4];
+#define WINFO(i, v)                                                                      \
+  do {                                                                                   \
+    if ((threadIdx.x & 63) == 0 && blockIdx.y == 0)                                      \
+      g_wave_info[blockIdx.x & 8191][threadIdx.x >> 6][i] += (unsigned)(v);              \
+  } while (0)
+#else
+#define WINFO(i, v) do {} while (0)
+#endif
+typedef const float4 __attribute__((address_space(3))) LF4;
+typedef const Coef32 __attribute__((address_space(3))) LC32;
+struct Stage {
+  LF4 *env;    // [blocks] envelopes (the Coef w-rows' first 16 B)
+  LC32 *c32;   // [blocks] block-local fp32 blocks
+};
+constexpr int kStageBlocks = 224;  // blocks of both mixtures a workgroup stages (32 KB)
+struct StageSmem {
+  float4 env[kStageBlocks];
+  Coef32 c32[kStageBlocks];
+};
+__device__ __forceinline__ void load_block32_lds(LC32 *__restrict__ rb, uint32_t j, CoefGroup32 &g) {
+  LC32 *b = rb + j;
+  g.m = b->center;
+  g.A = b->base;
+#pragma unroll
+  for (int q = 0; q < kGroup; ++q) {
+    g.a[q] = b->a[q];
+    g.b[q] = b->b[q];
+    g.c[q] = b->c[q];
+  }
+}
+// the envelope of the block starting at component k0 (global table or stage)
+template <bool STG>
+__device__ __forceinline__ float4 block_env(const double *tb, const Stage &st, int k0) {
+  if constexpr (STG) {
+    const float __attribute__((address_space(3))) *e =
+        (const float __attribute__((address_space(3))) *)(st.env + (k0 >> 3));
+    return make_float4(e[0], e[1], e[2], e[3]);
+  }
+  else return *reinterpret_cast<const float4 *>(tb + coef_off(k0, 3));
 }
 
 // the lowest set bit of m, or 0 when m is empty (the caller then reloads
@@ -342,12 +408,12 @@ __device__ __forceinline__ void lse_fold_z(const float (&z)[KR][kGroup], float A
 // F32 (prune mode 3): blocks that are not wide take lse_terms_z / lse_fold_z in the
 // pipelined loop, wide ones (the sign of their envelope's a^2) the fp64 fold
 // in a second loop after each round.
-template <int KR, bool CENSUS, int STRIDE = kWaves, bool F32 = false>
+template <int KR, bool CENSUS, int STRIDE = kWaves, bool F32 = false, bool STG = false>
 __device__ __forceinline__ void lse_chunks(KDbl *__restrict__ cs, const Coef *__restrict__ cv,
                                            int c0, int nb, const double (&y)[KR],
                                            LseAcc (&out)[KR], bool prune, LseWindow win,
                                            int nvalid, LseCensus &cen,
-                                           KC32 *__restrict__ c32 = nullptr) {
+                                           KC32 *__restrict__ c32 = nullptr, Stage stg = {}) {
   const int lane = threadIdx.x & 63;
   double m[KR], s[KR], y2[KR];
 #pragma unroll
@@ -359,7 +425,7 @@ __device__ __forceinline__ void lse_chunks(KDbl *__restrict__ cs, const Coef *__
     bool live = has, wide = false;
     if ((prune || F32) && has) {
       const double *t = reinterpret_cast<const double *>(cv);
-      const float4 e = *reinterpret_cast<const float4 *>(t + coef_off(k0, 3));
+      const float4 e = block_env<STG>(t, stg, k0);
       if (prune) live = envelope_bound(e, win) >= win.thr;
       wide = __builtin_signbit(e.w);
     }
@@ -381,6 +447,7 @@ __device__ __forceinline__ void lse_chunks(KDbl *__restrict__ cs, const Coef *__
       }
     }
     uint64_t mk = __ballot(live && !(F32 && wide));
+    if (STRIDE == 1) WINFO(3, __builtin_popcountll(__ballot(live)));
     // live blocks in order (the padding components of a last block have
     // alpha = -inf, make_coef_pad, so no tail masking is needed);
     // software-pipelined: the next live block's coefficients are loaded into
@@ -391,13 +458,17 @@ __device__ __forceinline__ void lse_chunks(KDbl *__restrict__ cs, const Coef *__
     bool have = next_live<STRIDE>(mk, r0, kg);
     if constexpr (F32) {
       CoefGroup32 g32;
-      if (have) load_group32(c32, kg, g32);
+      if (have) {
+        if constexpr (STG) load_block32_lds(stg.c32, (unsigned)kg >> 3, g32);
+        else load_group32(c32, kg, g32);
+      }
       while (have) {
         float z[KR][kGroup];
         lse_terms_z<KR>(g32, y, z);
         const float A = g32.A;
         have = next_live<STRIDE>(mk, r0, kg);
-        load_group32(c32, kg, g32);
+        if constexpr (STG) load_block32_lds(stg.c32, (unsigned)kg >> 3, g32);
+        else load_group32(c32, kg, g32);
         __builtin_amdgcn_sched_barrier(0);
         lse_fold_z<KR>(z, A, m, s);
       }
@@ -522,13 +593,14 @@ __device__ __forceinline__ void lse_terms_f32(const CoefGroup32 &g, float Mf,
   }
 }
 
-template <int KR, bool CENSUS, int STRIDE = kWaves, bool F32 = false>
+template <int KR, bool CENSUS, int STRIDE = kWaves, bool F32 = false, bool STG = false>
 __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
                                                    const Coef *__restrict__ cv, int c0, int nb,
                                                    const double (&y)[KR], const bool (&valid)[KR],
                                                    LseAcc (&out)[KR], LseWindow win, int nvalid,
                                                    LseCensus &cen, KC32 *__restrict__ c32 = nullptr,
-                                                   const CoefM *__restrict__ cmv = nullptr) {
+                                                   const CoefM *__restrict__ cmv = nullptr,
+                                                   Stage stg = {}) {
   const int lane = threadIdx.x & 63;
   const int nch = (nb + kChunk - 1) / kChunk;
   const double *tb = reinterpret_cast<const double *>(cv);
@@ -538,7 +610,7 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
   for (int r0 = c0; r0 < nch; r0 += STRIDE * 32) {
     const int k0 = round_k<STRIDE>(r0, lane);
     if (r0 + STRIDE * (lane >> 1) < nch && k0 < nb) {
-      const float b = envelope_bound(*reinterpret_cast<const float4 *>(tb + coef_off(k0, 3)), win);
+      const float b = envelope_bound(block_env<STG>(tb, stg, k0), win);
       if (b >= win.thr && b > bmax) { bmax = b; barg = k0; }
     }
   }
@@ -584,6 +656,7 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
 #pragma unroll
   for (int r = 0; r < KR; ++r) y2[r] = y[r] * y[r];
   for (int attempt = 0;; ++attempt) {
+    WINFO(1, 1);
 #pragma unroll
     for (int r = 0; r < KR; ++r) s[r] = 0.0;
     for (int r0 = c0; r0 < nch; r0 += STRIDE * 32) {
@@ -592,7 +665,7 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
       bool live = false, wide = false;
       float bnd = -INFINITY;  // the block's envelope bound over the window
       if (has) {
-        const float4 e = *reinterpret_cast<const float4 *>(tb + coef_off(k0, 3));
+        const float4 e = block_env<STG>(tb, stg, k0);
         bnd = envelope_bound(e, win);
         live = bnd >= win.thr;
         wide = __builtin_signbit(e.w);
@@ -619,6 +692,7 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
       // (mode 3: the live wide blocks -- kF32Spread, flagged by the sign of
       // their envelope's a^2 -- go to a second, fp64 loop after the round)
       uint64_t mk = __ballot(live && !(F32 && wide));
+      WINFO(0, __builtin_popcountll(__ballot(live)));
       // software-pipelined as in lse_chunks
       int kg = 0;
       bool have = next_live<STRIDE>(mk, r0, kg);
@@ -627,11 +701,13 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
         // order; one bit scan and a 32-bit offset per block (SALU)
         const float Mf = (float)M;  // an integer (< 2^24 in magnitude): exact
         KC32 *rb = c32 + 2 * r0;
+        LC32 *rbl = STG ? stg.c32 + 2 * r0 : nullptr;
         // chunks in the moment form (CoefM): lane 2i tests chunk r0 + i -- its
         // sigmas equal and x = |v| xh <= kMomXLim over the wave's whole
         // candidate range -- and the chunk is taken when either of its two
         // blocks is live; its blocks then leave the pair and wide loops
-        // (the moment form packs the lane's two candidate rows: two-row tiles only)
+        // (the moment form packs the lane's two candidate rows, or two chunks
+        // of its one row in one-row tiles)
         constexpr uint64_t kEven = 0x5555555555555555ull;
         // Eligibility: the truncation bound tau(x) = x^(D+1) / (D+1)! e^x (D =
         // kMomDeg) relative to the chunk's terms, which are at most 2^bound
@@ -644,7 +720,7 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
         // e^(2x) bounded)
         const float bnd1 = __builtin_bit_cast(float, dpp<kDppXor1>(__builtin_bit_cast(int, bnd)));
         bool elig = false;
-        if (KR == 2 && cmv && has && !(lane & 1)) {
+        if (cmv && has && !(lane & 1)) {
           const CoefM *q = cmv + (r0 + (lane >> 1));
           const float cf = (float)q->center;
           const float x = fmaxf(fabsf(win.lo - cf), fabsf(win.hi - cf)) * q->xh;
@@ -701,11 +777,33 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
 #pragma unroll
             for (int r = 0; r < KR; ++r) s[r] += (double)(b0[r] + b1[r]);
           }
+        } else {
+          // one row: chunks in pairs (the second of an odd last pair is chunk
+          // 0 of the round again, a valid address, its sum dropped)
+          KCM *rm = uniform_ptrm(cmv) + r0;
+          uint64_t cm = cmask;
+          while (cm) {
+            MomGroup ga, gb;
+            load_mom(rm, low_bit(cm) >> 1, ga);
+            cm &= cm - 1;
+            const bool two = cm != 0;
+            load_mom(rm, low_bit(cm) >> 1, gb);
+            cm &= cm - 1;
+            f2v a2, p2;
+            mom_terms2(ga, gb, Mf, y[0], a2, p2);
+            float b2[2];
+            mom_sum(a2, p2, b2);
+            s[0] += (double)(two ? b2[0] + b2[1] : b2[0]);
+          }
         }
         uint64_t m = __ballot(live && !wide) & ~cover;
         bool hv = m != 0;
         CoefGroup32 g32;
-        if (hv) load_block32(rb, low_bit(m), g32);
+        auto ld32 = [&](uint32_t j) {
+          if constexpr (STG) load_block32_lds(rbl, j, g32);
+          else load_block32(rb, j, g32);
+        };
+        if (hv) ld32(low_bit(m));
         // two live blocks per iteration: their fp32 sums (terms <= 1, 16 of
         // them) are added in fp32 and converted once (tools/fp32_pair_error.py
         // blockf32_uu_pair: 2.3e-8 relative at config 4 against 2.2e-8)
@@ -714,7 +812,7 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
           lse_terms_f32<KR>(g32, Mf, y, d);
           m &= m - 1;
           hv = m != 0;
-          load_block32(rb, low_bit(m), g32);
+          ld32(low_bit(m));
           __builtin_amdgcn_sched_barrier(0);
           lse_block_sum<KR>(d, b0);
           if (!hv) {
@@ -726,7 +824,7 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
           lse_terms_f32<KR>(g32, Mf, y, d);
           m &= m - 1;
           hv = m != 0;
-          load_block32(rb, low_bit(m), g32);
+          ld32(low_bit(m));
           __builtin_amdgcn_sched_barrier(0);
           lse_block_sum<KR>(d, b1);
 #pragma unroll
@@ -1013,9 +1111,10 @@ __device__ unsigned long long g_score_stamps[8192][4];
             (__builtin_amdgcn_s_getreg(63488 | 4) & 0xffff);                             \
     }                                                                                    \
   } while (0)
-// per wave (wave tiles): start and end of the component loops, lane 0 of
+// per wave (wave tiles): start and end of the component loops ([0], [1]),
+// after the candidate loads ([2]) and after the below mixture ([3]), lane 0 of
 // every wave of the blocks of suggestion 0
-__device__ unsigned long long g_wave_stamps[8192][kWaves][2];
+__device__ unsigned long long g_wave_stamps[8192][kWaves][4];
 #define WSTAMP(i)                                                                        \
   do {                                                                                   \
     if ((threadIdx.x & 63) == 0 && blockIdx.y == 0)                                      \
@@ -1026,15 +1125,21 @@ __device__ unsigned long long g_wave_stamps[8192][kWaves][2];
 #define WSTAMP(i) do {} while (0)
 #endif
 
-struct ScoreSmem {
-  double2 wpart[2][kWaves][kRMax][64];  // per-wave partials (below, above)
-  double2 merged[2][kRMax][64];         // merged per (mixture, candidate row)
+template <int R>
+struct ScoreSmemT {
+  double2 wpart[2][kWaves][R][64];      // per-wave partials (below, above)
+  double2 merged[2][R][64];             // merged per (mixture, candidate row)
   double best_s[kWaves], best_v[kWaves];  // wave tiles: each wave's argmax
   int64_t best_i[kWaves];
 #ifdef TPE_REREAD
   int64_t best_li[kWaves];
 #endif
   uint32_t arrive;                      // wave tiles: waves done with the tile
+};
+typedef ScoreSmemT<kRMax> ScoreSmem;
+// k_score_wave1: one candidate row, and the staged tables beside it
+struct ScoreSmem1 : ScoreSmemT<1> {
+  StageSmem stg;
 };
 
 #ifdef TPE_REREAD
@@ -1055,9 +1160,12 @@ __device__ unsigned long long g_rr2_cnt[4];
 __device__ double g_rr2_ex[64][8];
 #endif
 
-template <int KIND, bool CENSUS>
-__device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, int slot, int tile,
+// (SM: ScoreSmem, or ScoreSmem1 for the one-row wave tiles, whose
+// workgroup stages both mixtures' tables in LDS when they fit kStageBlocks)
+template <int KIND, bool CENSUS, typename SM>
+__device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot, int tile,
                                            int ntiles, bool known_active) {
+  constexpr bool STAGE = std::is_same<SM, ScoreSmem1>::value;
   constexpr int KR = tile_rows(KIND);
   constexpr bool LSE = kind_lse(KIND);
   constexpr bool WT = tile_waves(KIND) > 1;  // wave tiles: own candidates, all components
@@ -1076,13 +1184,37 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
       A.results[(int64_t)s * A.n_hp + hp] = Partial{NAN, NAN, -1, 0, 0};
     return;
   }
+  const int64_t sb = 2 * (int64_t)hp, sa = sb + 1;
+  const MixInfo ib = A.info[sb], ia = A.info[sa];
+  // staged tables (one-row wave tiles): below blocks [0, nbb), above after
+  const int nbb = (ib.K + kCoefBlock - 1) / kCoefBlock, nba = (ia.K + kCoefBlock - 1) / kCoefBlock;
+  bool staged = false;
   if constexpr (WT) {  // the block's arrival counter (finalize), before any wave can arrive
     if (threadIdx.x == 0) sm.arrive = 0u;
+    if constexpr (STAGE) {
+      staged = nbb + nba <= kStageBlocks && A.lse_prune > 2;  // block-uniform
+      if (staged) {
+        // 16-B units: per block its envelope, then its Coef32 (8 units)
+        const float4 *gb = reinterpret_cast<const float4 *>(A.coef + sb * A.kcap);
+        const float4 *ga = reinterpret_cast<const float4 *>(A.coef + sa * A.kcap);
+        const float4 *cb32 = reinterpret_cast<const float4 *>(A.coef32 + sb * (A.kcap / kCoefBlock));
+        const float4 *ca32 = reinterpret_cast<const float4 *>(A.coef32 + sa * (A.kcap / kCoefBlock));
+        float4 *env = sm.stg.env;
+        float4 *c32 = reinterpret_cast<float4 *>(sm.stg.c32);
+        for (int u = threadIdx.x; u < 9 * (nbb + nba); u += blockDim.x) {
+          const int b = u / 9, part = u - 9 * b;
+          const bool above = b >= nbb;
+          const int bl = above ? b - nbb : b;
+          if (part == 0)  // the w-row of block bl: 16 float4 per block, the envelope at 12
+            env[b] = (above ? ga : gb)[(int64_t)bl * 16 + 12];
+          else
+            c32[(int64_t)b * 8 + part - 1] = (above ? ca32 : cb32)[(int64_t)bl * 8 + part - 1];
+        }
+      }
+    }
     __syncthreads();
     WSTAMP(0);
   }
-  const int64_t sb = 2 * (int64_t)hp, sa = sb + 1;
-  const MixInfo ib = A.info[sb], ia = A.info[sa];
   const Coef *__restrict__ cb = A.coef + sb * A.kcap;
   const Coef *__restrict__ ca = A.coef + sa * A.kcap;
   const int64_t coff = (int64_t)s * A.cand_sstride + (int64_t)(A.cand_slot0 + slot) * A.n_cand;
@@ -1176,12 +1308,25 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
     if constexpr (LSE) {
       if (A.lse_prune != 0) rg = lse_range<KR>(y, valid);
     }
+    if constexpr (WT) WSTAMP(2);
 #pragma unroll
     for (int mix = 0; mix < 2; ++mix) {
       const Coef *__restrict__ cm = mix ? ca : cb;
       const int K = mix ? ia.K : ib.K;
       if constexpr (LSE) {
         const bool prune = A.lse_prune != 0;
+        // a wave without a valid candidate (the tail of a partial sort block:
+        // li >= n_cand on every lane) has nothing to sum; its rows are never
+        // read, so it keeps the empty sum instead of running an unpruned
+        // loop over every block (lse_window: no range, no threshold)
+        if (prune && !rg.any) {
+          if constexpr (WT) {
+#pragma unroll
+            for (int r = 0; r < KR; ++r)
+              sm.wpart[mix][wave][r][lane] = make_double2(lacc[mix][r].m, lacc[mix][r].s);
+          }
+          continue;
+        }
         LseWindow win{0.0f, 0.0f, -INFINITY};
         if (prune) win = lse_window<KR>(uniform_ptr(cm), mix ? ia.probe : ib.probe, K, y, valid, rg);
         // shifted single-exponent loop when the wave's window allows it
@@ -1194,8 +1339,18 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
         constexpr int ST = WT ? 1 : kWaves;
         const int cw0 = WT ? 0 : wv;
         bool shifted = false;
+        Stage stv{};
+        if constexpr (STAGE) {
+          stv.env = (LF4 *)(sm.stg.env + (mix ? nbb : 0));
+          stv.c32 = (LC32 *)(sm.stg.c32 + (mix ? nbb : 0));
+        }
         if (prune && A.lse_prune > 1 && K >= A.lse_shift_min && win.thr > -INFINITY) {
-          if (A.lse_prune > 2)  // block-local fp32 pairs (Coef32), moment chunks (CoefM)
+          if (STAGE && staged)  // (prune mode 3 only: the staged blocks are Coef32)
+            shifted = lse_chunks_shifted<KR, CENSUS, ST, true, STAGE>(
+                uniform_ptr(cm), cm, cw0, K, y, valid, lacc[mix], win, nvalid, lcen,
+                uniform_ptr32(A.coef32 + (mix ? sa : sb) * (A.kcap / kCoefBlock)),
+                A.lse_mom ? A.coefm + (mix ? sa : sb) * mom_stride(A.kcap) : nullptr, stv);
+          else if (A.lse_prune > 2)  // block-local fp32 pairs (Coef32), moment chunks (CoefM)
             shifted = lse_chunks_shifted<KR, CENSUS, ST, true>(
                 uniform_ptr(cm), cm, cw0, K, y, valid, lacc[mix], win, nvalid, lcen,
                 uniform_ptr32(A.coef32 + (mix ? sa : sb) * (A.kcap / kCoefBlock)),
@@ -1205,6 +1360,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
                                                          lacc[mix], win, nvalid, lcen);
         }
         if (!shifted) {
+          if (WT && prune && A.lse_prune > 1 && K >= A.lse_shift_min && win.thr > -INFINITY) WINFO(2, 1);
           if constexpr (WT) {
             // the exact per-group-lift loop over every chunk in order, one
             // pass (64 consecutive chunks per envelope round).  (Round 2 ran
@@ -1214,7 +1370,11 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
             // ~3 live blocks per pass.  Nothing compares the two tile shapes
             // bit for bit: batched, sharded and chunked runs of one draw take
             // the same tile shape.)
-            if (A.lse_prune > 2 || A.lse_f32)  // block-local fp32 (Coef32) where the block allows it
+            if (STAGE && staged)
+              lse_chunks<KR, CENSUS, 1, true, STAGE>(
+                  uniform_ptr(cm), cm, 0, K, y, lacc[mix], prune, win, nvalid, lcen,
+                  uniform_ptr32(A.coef32 + (mix ? sa : sb) * (A.kcap / kCoefBlock)), stv);
+            else if (A.lse_prune > 2 || A.lse_f32)  // block-local fp32 (Coef32) where the block allows it
               lse_chunks<KR, CENSUS, 1, true>(
                   uniform_ptr(cm), cm, 0, K, y, lacc[mix], prune, win, nvalid, lcen,
                   uniform_ptr32(A.coef32 + (mix ? sa : sb) * (A.kcap / kCoefBlock)));
@@ -1236,6 +1396,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, ScoreSmem &sm, in
 #pragma unroll
           for (int r = 0; r < KR; ++r)
             sm.wpart[mix][wave][r][lane] = make_double2(lacc[mix][r].m, lacc[mix][r].s);
+          if (mix == 0) WSTAMP(3);
         }
       } else {
         erf_chunks<KR, LOGN, CENSUS>(uniform_ptr(cm), wv, K, ub, lb, valid, wlo, whi, exact, pacc[mix], cen);
@@ -1566,6 +1727,16 @@ extern "C" int tpe_debug_score_stamps(unsigned long long *out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(tpe::g_score_stamps), sizeof(tpe::g_score_stamps)) ==
                  hipSuccess ? 0 : -5;
 }
+extern "C" int tpe_debug_wave_info(unsigned *out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(tpe::g_wave_info), sizeof(tpe::g_wave_info)) ==
+                 hipSuccess
+             ? 0
+             : -1;
+}
+extern "C" int tpe_debug_wave_info_clear() {
+  static const unsigned zero[8192 * 8 * 4] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(tpe::g_wave_info), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
 extern "C" int tpe_debug_wave_stamps(unsigned long long *out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(tpe::g_wave_stamps), sizeof(tpe::g_wave_stamps)) ==
                  hipSuccess ? 0 : -5;
@@ -1615,8 +1786,8 @@ __device__ __forceinline__ void mark_inactive(const ScoreArgs &A, int s, int s0,
 // allocation -- the combined one keeps the most any kind needs).
 enum { kSetNoErf = 0, kSetAll = 1, kSetWave = 2, kSetWave1 = 3 };
 
-template <int SET, bool CENSUS>
-__device__ __forceinline__ void score_block(const ScoreArgs &A, ScoreSmem &sm) {
+template <int SET, bool CENSUS, typename SM>
+__device__ __forceinline__ void score_block(const ScoreArgs &A, SM &sm) {
   const int b = blockIdx.x;
   int g = 0;
   while (g + 1 < A.n_groups && b >= A.grp_block0[g + 1]) ++g;
@@ -1633,29 +1804,29 @@ __device__ __forceinline__ void score_block(const ScoreArgs &A, ScoreSmem &sm) {
   }
   const bool known = A.compact != 0;
   if constexpr (SET == kSetWave) {
-    if (A.grp_kind[g] == KIND_LSE_LW) score_tile<KIND_LSE_LW, CENSUS>(A, sm, slot, tile, nt, known);
-    else score_tile<KIND_LSE_GW, CENSUS>(A, sm, slot, tile, nt, known);
+    if (A.grp_kind[g] == KIND_LSE_LW) score_tile<KIND_LSE_LW, CENSUS, SM>(A, sm, slot, tile, nt, known);
+    else score_tile<KIND_LSE_GW, CENSUS, SM>(A, sm, slot, tile, nt, known);
     return;
   } else if constexpr (SET == kSetWave1) {
-    if (A.grp_kind[g] == KIND_LSE_LW1) score_tile<KIND_LSE_LW1, CENSUS>(A, sm, slot, tile, nt, known);
-    else score_tile<KIND_LSE_GW1, CENSUS>(A, sm, slot, tile, nt, known);
+    if (A.grp_kind[g] == KIND_LSE_LW1) score_tile<KIND_LSE_LW1, CENSUS, SM>(A, sm, slot, tile, nt, known);
+    else score_tile<KIND_LSE_GW1, CENSUS, SM>(A, sm, slot, tile, nt, known);
     return;
   } else {
     switch (A.grp_kind[g]) {
-      case KIND_LSE_G: score_tile<KIND_LSE_G, CENSUS>(A, sm, slot, tile, nt, known); break;
-      case KIND_LSE_L: score_tile<KIND_LSE_L, CENSUS>(A, sm, slot, tile, nt, known); break;
-      case KIND_LSE_G1: score_tile<KIND_LSE_G1, CENSUS>(A, sm, slot, tile, nt, known); break;
-      case KIND_LSE_L1: score_tile<KIND_LSE_L1, CENSUS>(A, sm, slot, tile, nt, known); break;
-      case KIND_LSE_GW: score_tile<KIND_LSE_GW, CENSUS>(A, sm, slot, tile, nt, known); break;
-      case KIND_LSE_LW: score_tile<KIND_LSE_LW, CENSUS>(A, sm, slot, tile, nt, known); break;
+      case KIND_LSE_G: score_tile<KIND_LSE_G, CENSUS, SM>(A, sm, slot, tile, nt, known); break;
+      case KIND_LSE_L: score_tile<KIND_LSE_L, CENSUS, SM>(A, sm, slot, tile, nt, known); break;
+      case KIND_LSE_G1: score_tile<KIND_LSE_G1, CENSUS, SM>(A, sm, slot, tile, nt, known); break;
+      case KIND_LSE_L1: score_tile<KIND_LSE_L1, CENSUS, SM>(A, sm, slot, tile, nt, known); break;
+      case KIND_LSE_GW: score_tile<KIND_LSE_GW, CENSUS, SM>(A, sm, slot, tile, nt, known); break;
+      case KIND_LSE_LW: score_tile<KIND_LSE_LW, CENSUS, SM>(A, sm, slot, tile, nt, known); break;
       case KIND_ERF_G:
-        if constexpr (SET == kSetAll) score_tile<KIND_ERF_G, CENSUS>(A, sm, slot, tile, nt, known);
+        if constexpr (SET == kSetAll) score_tile<KIND_ERF_G, CENSUS, SM>(A, sm, slot, tile, nt, known);
         break;
       case KIND_ERF_L:
-        if constexpr (SET == kSetAll) score_tile<KIND_ERF_L, CENSUS>(A, sm, slot, tile, nt, known);
+        if constexpr (SET == kSetAll) score_tile<KIND_ERF_L, CENSUS, SM>(A, sm, slot, tile, nt, known);
         break;
-      case KIND_LAT: score_tile<KIND_LAT, CENSUS>(A, sm, slot, tile, nt, known); break;
-      default: score_tile<KIND_CAT, CENSUS>(A, sm, slot, tile, nt, known); break;
+      case KIND_LAT: score_tile<KIND_LAT, CENSUS, SM>(A, sm, slot, tile, nt, known); break;
+      default: score_tile<KIND_CAT, CENSUS, SM>(A, sm, slot, tile, nt, known); break;
     }
   }
 }
@@ -1681,7 +1852,7 @@ void k_score_wave(ScoreArgs A) {
 template <bool CENSUS>
 __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(TPE_WAVE_EU)))
 void k_score_wave1(ScoreArgs A) {
-  __shared__ ScoreSmem sm;
+  __shared__ ScoreSmem1 sm;
   score_block<kSetWave1, CENSUS>(A, sm);
 }
 

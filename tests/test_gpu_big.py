@@ -77,8 +77,13 @@ def test_config4_full_draw_shard_merge(cfg4_plan, cut):
     if cut % E.SHARD_ALIGN == 0:
         np.testing.assert_array_equal(merged.view(np.uint8), full.view(np.uint8))
     else:
+        # (the second shard's sort blocks start at the cut: every wave window
+        # there differs, and with it the wave exponent and which chunks take
+        # the moment form, so near-tied winners may flip; each flip is
+        # checked above to tie within the scoring tolerance -- the bound
+        # only guards against a systematic mismatch)
         ties = assert_winners_match(merged, full, msg='cfg4 shard merge')
-        assert ties <= 2, ties
+        assert ties <= 5, ties
     assert (full['index'] >= 0).all() and (full['index'] < n).all()
     assert np.all((full['value'] >= -5) & (full['value'] < 5))
 

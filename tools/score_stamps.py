@@ -42,6 +42,9 @@ def main(cfg, n_cand):
             plan.suggest([7 + i], n_cand, fetch=False)
         else:
             for l in range(lv + 1):
+                if i == 4 and l == lv and hasattr(eng.lib, 'tpe_debug_wave_info_clear'):
+                    eng.lib.tpe_synchronize(eng.h)
+                    assert eng.lib.tpe_debug_wave_info_clear() == 0
                 plan.suggest([7 + i], n_cand, level=l, fetch=False)
     eng.lib.tpe_synchronize(eng.h)
     buf = (C.c_ulonglong * (8192 * 4))()
@@ -64,9 +67,9 @@ def main(cfg, n_cand):
               (sl, (slot == sl).sum(), r[:, 0].min(), r[:, 0].max(), (r[:, 1] - r[:, 0]).mean(),
                (r[:, 1] - r[:, 0]).max(), (r[:, 2] - r[:, 1]).mean(), r[:, 2].max()))
     # per wave (wave tiles): component-loop durations and the block ends
-    wb = (C.c_ulonglong * (8192 * 8 * 2))()
+    wb = (C.c_ulonglong * (8192 * 8 * 4))()
     if hasattr(eng.lib, 'tpe_debug_wave_stamps') and eng.lib.tpe_debug_wave_stamps(wb) == 0:
-        ws = np.frombuffer(wb, dtype=np.uint64).reshape(8192, 8, 2).astype(np.int64)[:nb]
+        ws = np.frombuffer(wb, dtype=np.uint64).reshape(8192, 8, 4).astype(np.int64)[:nb]
         okw = (ws[:, :, 0] > 0) & (ws[:, :, 1] >= ws[:, :, 0])
         if okw.any():
             t0 = t[:, 0].min()
@@ -79,12 +82,49 @@ def main(cfg, n_cand):
                                                           np.quantile(d, 0.9), d.max(),
                                                           start[okw].min(), start[okw].max(),
                                                           end[okw].max()))
+            # block start (wave 0 entry) to each wave's start after the staging barrier
+            bst = rel[:, 0]
+            wst = np.where(okw, start, np.nan)
+            dl = wst - bst[:, None]
+            print('barrier delay (wave start - block entry): p50 %.1f p90 %.1f max %.1f us; '
+                  'block entries p50 %.1f max %.1f' % (np.nanmedian(dl), np.nanquantile(dl, 0.9),
+                                                       np.nanmax(dl), np.median(bst), bst.max()))
+            key0 = xcc * 64 + se * 16 + cu
+            bl = np.nanmax(dl, axis=1)
+            for b in np.argsort(np.nan_to_num(bl, nan=-1))[::-1][:8]:
+                same = np.where(key0 == key0[b])[0]
+                print('  block %4d delay %5.1f us entry %5.1f  cu-mates %s entries %s ends %s' % (
+                    b, bl[b], bst[b], same.tolist(), np.round(bst[same], 1).tolist(),
+                    np.round(np.where(okw[same], end[same], -1).max(axis=1), 1).tolist()))
             bend = np.where(okw, end, -1).max(axis=1)
             sel = bend >= 0
             print('block ends (last wave loop): mean %.1f us, max %.1f us (max / mean %.2f)' %
                   (bend[sel].mean(), bend[sel].max(), bend[sel].max() / bend[sel].mean()))
             # loop time by the wave's place in its 4096-candidate sort block
             # (dense value windows), from the tile mapping of tpe_score.hip
+            if (ws[:, :, 2:] > 0).all(axis=2)[okw].any():
+                ok4 = okw & (ws[:, :, 2] > 0) & (ws[:, :, 3] > 0)
+                ph = [(ws[:, :, 2] - ws[:, :, 0]), (ws[:, :, 3] - ws[:, :, 2]),
+                      (ws[:, :, 1] - ws[:, :, 3])]
+                for nm, a in zip(['candidates', 'below mixture', 'above mixture'], ph):
+                    a = a[ok4] / 100.0
+                    print('  %-14s mean %6.2f us  p50 %6.2f  p90 %6.2f  max %6.2f' %
+                          (nm, a.mean(), np.median(a), np.quantile(a, 0.9), a.max()))
+            if hasattr(eng.lib, 'tpe_debug_wave_info') and lv >= 0:
+                ib = (C.c_uint * (8192 * 8 * 4))()
+                assert eng.lib.tpe_debug_wave_info(ib) == 0
+                wi = np.frombuffer(ib, dtype=np.uint32).reshape(8192, 8, 4)[:nb].astype(np.int64)
+                dd = np.where(okw, dur, -1.0)
+                order = np.argsort(dd.ravel())[::-1]
+                print('per-wave work [shifted blocks, attempts, fallbacks, exact blocks] by loop time:')
+                for q, nm in [(0.5, 'p50'), (0.9, 'p90')]:
+                    sel = okw & (dur >= np.quantile(d, q - 0.05)) & (dur <= np.quantile(d, q + 0.05))
+                    print('  %s band: mean %s' % (nm, np.round(wi[sel].mean(axis=0), 1).tolist()))
+                for f in order[:12]:
+                    b, w = divmod(int(f), 8)
+                    print('  block %4d wave %d  %6.1f us  %s  phases %s' % (
+                        b, w, dur[b, w], wi[b, w].tolist(),
+                        np.round((ws[b, w, [2, 3, 1]] - ws[b, w, [0, 2, 3]]) / 100.0, 1).tolist()))
             hist = np.histogram(d, bins=[0, 2, 5, 10, 20, 40, 80, 1e9])[0]
             print('wave loop histogram (us: 0-2,2-5,5-10,10-20,20-40,40-80,80+):', hist.tolist())
     key = xcc * 64 + se * 16 + cu
