@@ -476,6 +476,15 @@ __device__ __forceinline__ void stable_bucket_scatter(const unsigned char *bk, i
 }
 
 
+// Lookup slots (categorical, value lattice) drawn inside the scoring tile
+// instead of by the sorted draw (ScoreArgs::lookup_draw): below mixtures of
+// 1 .. kFuseTab components, whose LDS table the tile builds (DrawTableT<
+// kFuseTab>; the table, hence every draw, is the one the draw kernels build
+// for that K).  Both kernels decide from the same device-side K.
+__device__ __forceinline__ bool lookup_inline(const ScoreArgs &A, int K) {
+  return A.lookup_draw && K >= 1 && K <= kFuseTab;
+}
+
 template <int CAP, int NT>
 struct SortedDrawLds {
   DrawTableT<CAP> T;

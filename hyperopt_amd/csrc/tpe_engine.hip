@@ -24,6 +24,15 @@ static int64_t chunk_budget();
 // TPE_SIDE_STREAMS=1: the lattice launch and a mixed level's lookup launch
 // run on auxiliary streams beside the draw / the wave-tile launch (fork and
 // join events); default off: every launch in order on the suggest stream
+// lookup slots drawn inside their scoring tiles (ScoreArgs::lookup_draw);
+// TPE_LOOKUP_DRAW=0 writes them from the sorted draw instead (A/B)
+static bool lookup_draw_on() {
+  static const bool on = [] {
+    const char *e = std::getenv("TPE_LOOKUP_DRAW");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
 static bool side_streams_on() {
   static const bool on = std::getenv("TPE_SIDE_STREAMS") != nullptr;
   return on;
@@ -127,6 +136,7 @@ struct tpe_plan {
   };
   StepKey graph_key, pending_key;
   bool graph_ok = false, pending = false;
+  bool capturing = false;  // enqueue_step under graph capture (no per-call patch of score seeds)
   hipGraph_t graph = nullptr;
   hipGraphExec_t graph_exec = nullptr;
   std::vector<hipGraphNode_t> fit_nodes, draw_nodes;
@@ -820,6 +830,10 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
     for (int i = 0; i < kInlineSeeds && i < n_sug; ++i) a.seed_inline[i] = p->h_seeds[i];
     a.n_inline_seeds = (int32_t)std::min<int64_t>(n_sug, kInlineSeeds);
     a.lse_pos = (sorted_draw || small_sort) ? 1 : 0;
+    // lookup slots drawn by their scoring tiles (no write / read-back of their
+    // candidates); not in a captured graph, whose replays patch the seeds of
+    // the draw nodes only
+    a.lookup_draw = sorted_draw && !p->capturing && lookup_draw_on() ? 1 : 0;
     a.lse_prune = (sorted_draw || small_sort) ? p->prune_mode : 0;
     a.lse_shift_min = lse_shift_min();
     // prune mode 3's block-local fp32 pairs on every log-sum-exp slot of the
@@ -1419,7 +1433,9 @@ int capture_step(tpe_engine *h, tpe_plan *p, int32_t nb, double prior_weight, in
                  int64_t n_sug, int64_t n_cand, hipStream_t st) {
   graph_reset(p);
   CKH(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+  p->capturing = true;
   const int rc = enqueue_step(h, p, nb, prior_weight, lf, n_sug, n_cand, st);
+  p->capturing = false;
   hipGraph_t g = nullptr;
   const hipError_t ec = hipStreamEndCapture(st, &g);
   if (rc || ec != hipSuccess || !g) {

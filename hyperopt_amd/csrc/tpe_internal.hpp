@@ -272,6 +272,9 @@ struct ScoreArgs {
                              // pairs (prune mode 3's arithmetic on small draws)
   int32_t lse_mom;           // prune mode 3 wave tiles take the moment form of eligible
                              // 16-component chunks (CoefM; TPE_MOMENT=0 switches it off)
+  int32_t lookup_draw;       // the sorted draw leaves the lookup slots (categorical, value
+                             // lattice) unwritten and the scoring tile draws them itself,
+                             // for below mixtures of 1 .. kFuseTab components (lookup_inline)
   const LatInfo *lat_info;   // [P] value lattices (KIND_LAT slots)
   const double2 *lat;        // lattice (lpdf below, lpdf above) pairs
 };

@@ -74,6 +74,8 @@ __device__ __forceinline__ void sorted_block(const ScoreArgs &A, int32_t *__rest
       !hp_active(A.hps[hp], A.results + (int64_t)s * A.n_hp, A.cond_parent, A.cond_branch))
     return;
   const int kind = slot_kind(A, slot);
+  // lookup slots the scoring tile draws itself: nothing to write
+  if (!EXT && (kind == KIND_CAT || kind == KIND_LAT) && lookup_inline(A, A.info[2 * hp].K)) return;
   sorted_block_body<CAP, NT, EXT>(
       A, slot, s, (int64_t)blockIdx.x * kSortedBlock,
       kind_lse(kind) || kind == KIND_ERF_G || kind == KIND_ERF_L, kind_logn(kind), pos_out, src,

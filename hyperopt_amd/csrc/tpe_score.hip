@@ -1135,6 +1135,7 @@ struct ScoreSmemT {
   int64_t best_li[kWaves];
 #endif
   uint32_t arrive;                      // wave tiles: waves done with the tile
+  DrawTableT<kFuseTab> dt;              // lookup tiles drawing their candidates (lookup_inline)
 };
 typedef ScoreSmemT<kRMax> ScoreSmem;
 // k_score_wave1: one candidate row, and the staged tables beside it
@@ -1162,7 +1163,7 @@ __device__ double g_rr2_ex[64][8];
 
 // (SM: ScoreSmem, or ScoreSmem1 for the one-row wave tiles, whose
 // workgroup stages both mixtures' tables in LDS when they fit kStageBlocks)
-template <int KIND, bool CENSUS, typename SM>
+template <int KIND, bool CENSUS, typename SM, bool LDRAW = false>
 __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot, int tile,
                                            int ntiles, bool known_active) {
   constexpr bool STAGE = std::is_same<SM, ScoreSmem1>::value;
@@ -1224,6 +1225,15 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
   const int32_t *__restrict__ cpos =
       ((ERF || (LSE && A.lse_pos)) && A.cand_pos) ? A.cand_pos + coff : nullptr;
 
+  // lookup slots drawn here (ScoreArgs::lookup_draw): the below mixture's
+  // draw table in LDS (block-wide, before any wave can arrive), then each
+  // candidate is the draw of its global index, as k_draw_sorted would have
+  // written it
+  bool ldraw = false;
+  if constexpr (LDRAW && (LAT || KIND == KIND_CAT)) {
+    ldraw = lookup_inline(A, ib.K);  // block-uniform
+    if (ldraw) build_table(H, ib.K, A.mw + sb * A.kcap, A.mmu + sb * A.kcap, A.msig + sb * A.kcap, sm.dt);
+  }
   int64_t li[KR];
   bool valid[KR];
   double x[KR], y[KR], ub[KR], lb[KR];
@@ -1247,7 +1257,23 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
   for (int r = 0; r < KR; ++r) {
     li[r] = wt0 + r * 64 + lane;
     valid[r] = li[r] < A.n_cand;
-    x[r] = valid[r] ? cand[li[r]] : (LOGN ? 1.0 : 0.0);
+    if constexpr (LDRAW && (LAT || KIND == KIND_CAT)) {
+      if (ldraw) {
+        const uint64_t gi = (uint64_t)(A.cand_begin + li[r]);
+        const uint64_t seed = suggestion_seed(A, s);
+        // (out of line, as in the draw kernels: inlined, its inverse CDFs
+        // would set the register allocation of the whole scoring kernel)
+        x[r] = valid[r] ? draw_table_ool<kFuseTab>(A.hps + hp, ib.K, A.mmu + sb * A.kcap,
+                                                   A.msig + sb * A.kcap, &sm.dt,
+                                                   draw_block0(seed, gi, (uint32_t)hp), seed, gi,
+                                                   (uint32_t)hp)
+                        : 0.0;
+      } else {
+        x[r] = valid[r] ? cand[li[r]] : 0.0;
+      }
+    } else {
+      x[r] = valid[r] ? cand[li[r]] : (LOGN ? 1.0 : 0.0);
+    }
     y[r] = ub[r] = lb[r] = 0.0;
     // candidate-side transforms, once per candidate
     if constexpr (LSE) {
@@ -1784,7 +1810,7 @@ __device__ __forceinline__ void mark_inactive(const ScoreArgs &A, int s, int s0,
 // erf ones, every kind, or only the wave-tile log-sum-exp kinds (levels of
 // large draws whose every slot is one: a kernel with only their register
 // allocation -- the combined one keeps the most any kind needs).
-enum { kSetNoErf = 0, kSetAll = 1, kSetWave = 2, kSetWave1 = 3 };
+enum { kSetNoErf = 0, kSetAll = 1, kSetWave = 2, kSetWave1 = 3, kSetLookup = 4 };
 
 template <int SET, bool CENSUS, typename SM>
 __device__ __forceinline__ void score_block(const ScoreArgs &A, SM &sm) {
@@ -1806,6 +1832,10 @@ __device__ __forceinline__ void score_block(const ScoreArgs &A, SM &sm) {
   if constexpr (SET == kSetWave) {
     if (A.grp_kind[g] == KIND_LSE_LW) score_tile<KIND_LSE_LW, CENSUS, SM>(A, sm, slot, tile, nt, known);
     else score_tile<KIND_LSE_GW, CENSUS, SM>(A, sm, slot, tile, nt, known);
+    return;
+  } else if constexpr (SET == kSetLookup) {
+    if (A.grp_kind[g] == KIND_LAT) score_tile<KIND_LAT, CENSUS, SM, true>(A, sm, slot, tile, nt, known);
+    else score_tile<KIND_CAT, CENSUS, SM, true>(A, sm, slot, tile, nt, known);
     return;
   } else if constexpr (SET == kSetWave1) {
     if (A.grp_kind[g] == KIND_LSE_LW1) score_tile<KIND_LSE_LW1, CENSUS, SM>(A, sm, slot, tile, nt, known);
@@ -1854,6 +1884,16 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(TPE
 void k_score_wave1(ScoreArgs A) {
   __shared__ ScoreSmem1 sm;
   score_block<kSetWave1, CENSUS>(A, sm);
+}
+
+// the lookup tiles (categorical, value lattice) that draw their own
+// candidates (ScoreArgs::lookup_draw) in a kernel of their own: the table
+// draw's call is kept out of the combined kernel's register allocation
+template <bool CENSUS>
+__global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(4)))
+void k_score_lookup(ScoreArgs A) {
+  __shared__ ScoreSmemT<1> sm;
+  score_block<kSetLookup, CENSUS>(A, sm);
 }
 
 // Value-lattice scoring of the bounded quantized hps (KIND_LAT).  A drawn
@@ -2063,12 +2103,20 @@ hipError_t launch_lattice_draw(const ScoreArgs &a, const int32_t *hps_of_level, 
 }
 
 // the groups of a (kind) subset of a launch's grid, renumbered
-static ScoreArgs select_groups(const ScoreArgs &a, bool wave_lse) {
+// the launch class of a kind group: 0 wave-tile log-sum-exp (k_score_wave /
+// k_score_wave1), 1 lookups drawing their own candidates (k_score_lookup),
+// 2 the rest (k_score)
+static int group_class(const ScoreArgs &a, int kind) {
+  if (kind_wave_lse(kind)) return 0;
+  if (a.lookup_draw && (kind == KIND_CAT || kind == KIND_LAT)) return 1;
+  return 2;
+}
+static ScoreArgs select_groups(const ScoreArgs &a, int cls) {
   ScoreArgs b = a;
   b.n_groups = 0;
   int32_t blocks = 0;
   for (int i = 0; i < a.n_groups; ++i) {
-    if (kind_wave_lse(a.grp_kind[i]) != wave_lse) continue;
+    if (group_class(a, a.grp_kind[i]) != cls) continue;
     const int j = b.n_groups++;
     b.grp_kind[j] = a.grp_kind[i];
     b.grp_slot0[j] = a.grp_slot0[i];
@@ -2081,42 +2129,24 @@ static ScoreArgs select_groups(const ScoreArgs &a, bool wave_lse) {
   return b;
 }
 
-hipError_t launch_score(const ScoreArgs &a, bool has_erf, hipStream_t st, hipStream_t side,
-                        hipEvent_t ev_fork, hipEvent_t ev_join) {
-  if (a.n_groups <= 0 || a.n_suggest <= 0) return hipSuccess;
+// one launch of a single class's groups
+static hipError_t launch_class(const ScoreArgs &a, int cls, bool has_erf, hipStream_t st) {
+  if (a.n_groups <= 0) return hipSuccess;
   const int blocks = a.grp_block0[a.n_groups];
   if (blocks <= 0) return hipSuccess;
-  bool any_wave = false, all_wave = true, one_row = false;
-  for (int i = 0; i < a.n_groups; ++i) {
-    const bool w = kind_wave_lse(a.grp_kind[i]);
-    any_wave |= w;
-    all_wave &= w;
-    one_row |= a.grp_kind[i] == KIND_LSE_GW1 || a.grp_kind[i] == KIND_LSE_LW1;
-  }
-  if (any_wave && !all_wave) {
-    // a level of wave-tile log-sum-exp slots and other kinds (lookups,
-    // quantized): the log-sum-exp groups run their own wave kernel, the rest
-    // the combined one -- beside it on the side stream when one is given
-    const ScoreArgs w = select_groups(a, true), o = select_groups(a, false);
-    hipError_t e;
-    if (side) {
-      if ((e = hipEventRecord(ev_fork, st)) != hipSuccess) return e;
-      if ((e = hipStreamWaitEvent(side, ev_fork, 0)) != hipSuccess) return e;
-    }
-    const hipError_t eo = launch_score(o, has_erf, side ? side : st, nullptr, nullptr, nullptr);
-    // (once forked, the side stream is joined back on every path)
-    const hipError_t ej = side ? hipEventRecord(ev_join, side) : hipSuccess;
-    const hipError_t ew = launch_score(w, false, st, nullptr, nullptr, nullptr);
-    if (side && ej == hipSuccess && (e = hipStreamWaitEvent(st, ev_join, 0)) != hipSuccess) return e;
-    return eo != hipSuccess ? eo : ej != hipSuccess ? ej : ew;
-  }
   const dim3 g((unsigned)blocks, a.n_suggest);
-  if (all_wave && one_row) {
+  bool one_row = false;
+  for (int i = 0; i < a.n_groups; ++i)
+    one_row |= a.grp_kind[i] == KIND_LSE_GW1 || a.grp_kind[i] == KIND_LSE_LW1;
+  if (cls == 0 && one_row) {
     if (a.census) k_score_wave1<true><<<g, kWaves * 64, 0, st>>>(a);
     else k_score_wave1<false><<<g, kWaves * 64, 0, st>>>(a);
-  } else if (all_wave) {
+  } else if (cls == 0) {
     if (a.census) k_score_wave<true><<<g, kWaves * 64, 0, st>>>(a);
     else k_score_wave<false><<<g, kWaves * 64, 0, st>>>(a);
+  } else if (cls == 1) {
+    if (a.census) k_score_lookup<true><<<g, kWaves * 64, 0, st>>>(a);
+    else k_score_lookup<false><<<g, kWaves * 64, 0, st>>>(a);
   } else if (has_erf) {
     if (a.census) k_score<true, true><<<g, kWaves * 64, 0, st>>>(a);
     else k_score<true, false><<<g, kWaves * 64, 0, st>>>(a);
@@ -2125,6 +2155,34 @@ hipError_t launch_score(const ScoreArgs &a, bool has_erf, hipStream_t st, hipStr
     else k_score<false, false><<<g, kWaves * 64, 0, st>>>(a);
   }
   return hipGetLastError();
+}
+
+hipError_t launch_score(const ScoreArgs &a, bool has_erf, hipStream_t st, hipStream_t side,
+                        hipEvent_t ev_fork, hipEvent_t ev_join) {
+  if (a.n_groups <= 0 || a.n_suggest <= 0) return hipSuccess;
+  if (a.grp_block0[a.n_groups] <= 0) return hipSuccess;
+  bool has[3] = {false, false, false};
+  for (int i = 0; i < a.n_groups; ++i) has[group_class(a, a.grp_kind[i])] = true;
+  const int ncls = (int)has[0] + (int)has[1] + (int)has[2];
+  if (ncls == 1) return launch_class(a, has[0] ? 0 : has[1] ? 1 : 2, has_erf, st);
+  // a level of several classes: one launch per class.  The wave-tile
+  // log-sum-exp launch on st; the others in order on st, or beside it on the
+  // side stream when one is given (TPE_SIDE_STREAMS)
+  hipError_t e;
+  const bool fork = side && has[0];
+  if (fork) {
+    if ((e = hipEventRecord(ev_fork, st)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(side, ev_fork, 0)) != hipSuccess) return e;
+  }
+  hipStream_t so = fork ? side : st;
+  hipError_t eo = hipSuccess;
+  for (int c = 1; c <= 2 && eo == hipSuccess; ++c)
+    if (has[c]) eo = launch_class(select_groups(a, c), c, has_erf, so);
+  // (once forked, the side stream is joined back on every path)
+  const hipError_t ej = fork ? hipEventRecord(ev_join, side) : hipSuccess;
+  const hipError_t ew = has[0] ? launch_class(select_groups(a, 0), 0, false, st) : hipSuccess;
+  if (fork && ej == hipSuccess && (e = hipStreamWaitEvent(st, ev_join, 0)) != hipSuccess) return e;
+  return eo != hipSuccess ? eo : ej != hipSuccess ? ej : ew;
 }
 
 }  // namespace tpe
