@@ -33,6 +33,15 @@ static bool lookup_draw_on() {
   }();
   return on;
 }
+// TPE_LOOKUP_FORK=0: a chunk's self-drawing lookup launch in order on the
+// suggest stream instead of beside its draw
+static bool lookup_fork_on() {
+  static const bool on = [] {
+    const char *e = std::getenv("TPE_LOOKUP_FORK");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
 static bool side_streams_on() {
   static const bool on = std::getenv("TPE_SIDE_STREAMS") != nullptr;
   return on;
@@ -605,7 +614,7 @@ FitArgs fit_args(tpe_plan *p, int32_t n_below, double prior_weight, int32_t lf) 
 }
 
 int score_launch(tpe_engine *h, tpe_plan *p, ScoreArgs a, bool has_erf, int64_t cn,
-                 hipStream_t sg, bool record) {
+                 hipStream_t sg, bool record, int classes = 7) {
   tpe_plan::Prof *pr = nullptr;
   if (record && p->prof_cap > 0) {
     pr = &p->prof[0];
@@ -615,7 +624,7 @@ int score_launch(tpe_engine *h, tpe_plan *p, ScoreArgs a, bool has_erf, int64_t 
   // (a level mixing wave-tile log-sum-exp slots with other kinds: those run
   // beside it on an auxiliary stream; the events are free at scoring time)
   CKH(launch_score(a, has_erf, sg, side_streams_on() ? h->aux[1] : nullptr, p->ev_join[1],
-                   p->ev_join[2]));
+                   p->ev_join[2], classes));
   if (pr) {
     CKH(hipEventRecord(pr->b[pr->n], sg));
     pr->pairs[pr->n] = (double)cn * (double)a.n_suggest;
@@ -840,6 +849,26 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
     // suggest, pruned (large draws) or not (small draws: every pair, 8-wave
     // component-split tiles)
     a.lse_f32 = p->prune_mode == 3 ? 1 : 0;
+    // lookup tiles drawing their own candidates need nothing from this
+    // chunk's draw: forked onto an auxiliary stream, they run beside the draw
+    // and the log-sum-exp scoring, and st waits for them before the next
+    // chunk (TPE_LOOKUP_FORK=0: in order on st)
+    const int cls = score_classes(a);
+    const bool lk_fork = (cls & 2) && (cls & ~2) && lookup_fork_on();
+    if (lk_fork) {
+      CKH(hipEventRecord(p->ev_join[3], st));
+      CKH(hipStreamWaitEvent(h->aux[2], p->ev_join[3], 0));
+      const hipError_t el = launch_score(a, erf_level, h->aux[2], nullptr, nullptr, nullptr, 2);
+      CKH(hipEventRecord(p->ev_join[4], h->aux[2]));
+      if (el != hipSuccess) {
+        (void)hipStreamWaitEvent(st, p->ev_join[4], 0);
+        return fail(h, TPE_E_HIP, "lookup launch");
+      }
+    }
+    // (every exit below joins the lookup stream back first)
+    auto join_lk = [&]() {
+      if (lk_fork) (void)hipStreamWaitEvent(st, p->ev_join[4], 0);
+    };
     if (fuse_draw) {
       tpe_plan::Prof *pr = nullptr;
       if (p->prof_cap > 0 && p->prof[1].n < p->prof_cap) pr = &p->prof[1];
@@ -852,7 +881,8 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
         pr->n++;
       }
     } else if (sorted_draw) {
-      CKH(launch_draw_sorted(a, kmax <= kFuseTab, p->d_cpos, st));
+      const hipError_t e = launch_draw_sorted(a, kmax <= kFuseTab, p->d_cpos, st);
+      if (e != hipSuccess) { join_lk(); return fail(h, TPE_E_HIP, hipGetErrorString(e)); }
     } else {
       CKH(launch_draw(a, table_draw, st));
     }
@@ -862,7 +892,8 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
       CKH(hipStreamWaitEvent(st, p->ev_join[0], 0));
       joined = true;
     }
-    rc = score_launch(h, p, a, erf_level, cn, st, true);
+    rc = score_launch(h, p, a, erf_level, cn, st, true, lk_fork ? 5 : 7);
+    join_lk();
     if (rc) return rc;
     c0 += cn;
   } while (c0 < n_cand);

@@ -319,9 +319,13 @@ hipError_t launch_prep(const tpe_hp *hps, int32_t n_hp, const double *mw,
 // a level mixing wave-tile log-sum-exp groups with other kinds runs two
 // launches: the other kinds on `side` between fork / join events (when side
 // is given; st waits for the join), the log-sum-exp groups on st
+// classes: bit mask of the launch classes to run (score_classes)
 hipError_t launch_score(const ScoreArgs &a, bool has_erf, hipStream_t st,
                         hipStream_t side = nullptr, hipEvent_t ev_fork = nullptr,
-                        hipEvent_t ev_join = nullptr);
+                        hipEvent_t ev_join = nullptr, int classes = 7);
+// the launch classes present among a launch's kind groups (bit c: class c;
+// 0 wave-tile log-sum-exp, 1 lookups drawing their own candidates, 2 the rest)
+int score_classes(const ScoreArgs &a);
 // lpdf pairs of every lattice point of the first n_lat hps of a level
 // (hps_of_level[], host arrays; one block of kLatThreads per point, up to
 // kLatJobs hps per launch), written to lat_out

@@ -720,7 +720,7 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
         // e^(2x) bounded)
         const float bnd1 = __builtin_bit_cast(float, dpp<kDppXor1>(__builtin_bit_cast(int, bnd)));
         bool elig = false;
-        if (cmv && has && !(lane & 1)) {
+        if (KR <= 2 && cmv && has && !(lane & 1)) {
           const CoefM *q = cmv + (r0 + (lane >> 1));
           const float cf = (float)q->center;
           const float x = fmaxf(fabsf(win.lo - cf), fabsf(win.hi - cf)) * q->xh;
@@ -777,7 +777,7 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
 #pragma unroll
             for (int r = 0; r < KR; ++r) s[r] += (double)(b0[r] + b1[r]);
           }
-        } else {
+        } else if constexpr (KR == 1) {
           // one row: chunks in pairs (the second of an odd last pair is chunk
           // 0 of the round again, a valid address, its sum dropped)
           KCM *rm = uniform_ptrm(cmv) + r0;
@@ -2157,14 +2157,25 @@ static hipError_t launch_class(const ScoreArgs &a, int cls, bool has_erf, hipStr
   return hipGetLastError();
 }
 
+int score_classes(const ScoreArgs &a) {
+  int m = 0;
+  for (int i = 0; i < a.n_groups; ++i) m |= 1 << group_class(a, a.grp_kind[i]);
+  return m;
+}
+
 hipError_t launch_score(const ScoreArgs &a, bool has_erf, hipStream_t st, hipStream_t side,
-                        hipEvent_t ev_fork, hipEvent_t ev_join) {
+                        hipEvent_t ev_fork, hipEvent_t ev_join, int classes) {
   if (a.n_groups <= 0 || a.n_suggest <= 0) return hipSuccess;
   if (a.grp_block0[a.n_groups] <= 0) return hipSuccess;
   bool has[3] = {false, false, false};
   for (int i = 0; i < a.n_groups; ++i) has[group_class(a, a.grp_kind[i])] = true;
+  for (int c = 0; c < 3; ++c) has[c] = has[c] && ((classes >> c) & 1);
   const int ncls = (int)has[0] + (int)has[1] + (int)has[2];
-  if (ncls == 1) return launch_class(a, has[0] ? 0 : has[1] ? 1 : 2, has_erf, st);
+  if (ncls == 0) return hipSuccess;
+  if (ncls == 1) {
+    const int c = has[0] ? 0 : has[1] ? 1 : 2;
+    return launch_class(score_classes(a) == (1 << c) ? a : select_groups(a, c), c, has_erf, st);
+  }
   // a level of several classes: one launch per class.  The wave-tile
   // log-sum-exp launch on st; the others in order on st, or beside it on the
   // side stream when one is given (TPE_SIDE_STREAMS)

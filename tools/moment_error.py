@@ -40,10 +40,10 @@ import big_configs  # noqa: E402
 
 LOG2E = 1.4426950408889634
 LN2 = math.log(2.0)
-P = 9           # degree (10 moments), tpe_internal.hpp kMomDeg
-X_LIM = 0.65    # x^(P+1)/(P+1)! e^x <= 7.1e-9, kMomXLim
-X_CAP = 2.5     # kMomXCap
-CH = 16         # components per chunk, kMomChunk
+P = int(os.environ.get('MOM_P', '9'))  # degree, tpe_internal.hpp kMomDeg
+X_LIM = float(os.environ.get('MOM_XLIM', '0.65'))  # x^(P+1)/(P+1)! e^x <= 7.1e-9, kMomXLim
+X_CAP = float(os.environ.get('MOM_XCAP', '2.5'))  # kMomXCap
+CH = int(os.environ.get('MOM_CH', '16'))  # components per chunk, kMomChunk
 
 
 def f32(x):
@@ -128,6 +128,9 @@ def score(B, y):
     with np.errstate(divide='ignore'):
         l2tau = (P + 1) * np.log2(x) + x * math.log2(math.e) - math.log2(math.factorial(P + 1))
     use = (x <= X_LIM) | ((x <= X_CAP) & (l2tau + bound <= L - dead))
+    live = bound >= L - dead - 1
+    score.live = getattr(score, 'live', 0) + int(live.sum())
+    score.live_mom = getattr(score, 'live_mom', 0) + int((live & use).sum())
     bs = np.empty((y.size, nb), np.float32)
     # moment blocks
     v = f32(y[:, None] - B['cen'][None, :])                       # (n, nb)
@@ -179,6 +182,8 @@ def main():
         err = np.abs(g - ref) / np.maximum(1.0, np.abs(ref))
         print('%-6s %s K=%d n=%d max rel %.3g  p99.9 %.3g  mean %.3g' % (
             name, cfg, w.size, xc.size, err.max(), np.quantile(err, 0.999), err.mean()))
+    print('live (wave, chunk) pairs %d, of them in the moment form %.3f' % (
+        score.live, score.live_mom / max(score.live, 1)))
     print('moment-form blocks: %.3f of the (wave, block) pairs; equal-sigma blocks %.3f; '
           'xh median %.3g' % (used / (nw * B['cen'].size), np.isfinite(B['xh']).mean(),
                               np.median(B['xh'][np.isfinite(B['xh'])]) if np.isfinite(B['xh']).any() else np.nan))
