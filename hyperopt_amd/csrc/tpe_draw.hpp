@@ -537,7 +537,7 @@ __device__ __forceinline__ void sorted_block_body(const ScoreArgs &A, int slot, 
       continue;
     }
     L.xs[i] = x;
-    const double key = lg ? log(x) : x;
+    const double key = lg ? fast_log(x) : x;
     if (fabs(key) < INFINITY) { lo = fmin(lo, key); hi = fmax(hi, key); }
   }
   if (!bucket) return;
@@ -555,7 +555,7 @@ __device__ __forceinline__ void sorted_block_body(const ScoreArgs &A, int slot, 
   for (int w = 0; w < NT / 64; ++w) { lo = fmin(lo, L.red[0][w]); hi = fmax(hi, L.red[1][w]); }
   const double scale = hi > lo ? (double)kSortBuckets / (hi - lo) : 0.0;
   for (int i = t; i < n; i += NT) {
-    const double key = lg ? log(L.xs[i]) : L.xs[i];
+    const double key = lg ? fast_log(L.xs[i]) : L.xs[i];
     int b = kSortBuckets - 1;
     if (fabs(key) < INFINITY) b = min(kSortBuckets - 1, max(0, (int)((key - lo) * scale)));
     L.bk[i] = (unsigned char)b;

@@ -140,7 +140,7 @@ __global__ __launch_bounds__(1024) void k_bucket(ScoreArgs A, int32_t slot_begin
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
     const double x = cand[i];
     xs[i] = x;
-    const double t = lg ? log(fmax(x, 1e-300)) : x;
+    const double t = lg ? fast_log(fmax(x, 1e-300)) : x;
     if (t == t && fabs(t) < INFINITY) { lo = fmin(lo, t); hi = fmax(hi, t); }
   }
 #pragma unroll
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(1024) void k_bucket(ScoreArgs A, int32_t slot_begin
   const double scale = hi > lo ? (double)kBuckets / (hi - lo) : 0.0;
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
     const double x = xs[i];
-    const double t = lg ? log(fmax(x, 1e-300)) : x;
+    const double t = lg ? fast_log(fmax(x, 1e-300)) : x;
     int b = kBuckets - 1;
     if (t == t && fabs(t) < INFINITY) b = min(kBuckets - 1, max(0, (int)((t - lo) * scale)));
     bk[i] = (unsigned char)b;

@@ -1277,7 +1277,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
     y[r] = ub[r] = lb[r] = 0.0;
     // candidate-side transforms, once per candidate
     if constexpr (LSE) {
-      y[r] = (LOGN ? log(x[r]) : x[r]) - H.prior_mu;
+      y[r] = (LOGN ? fast_log(x[r]) : x[r]) - H.prior_mu;
     } else if constexpr (ERF) {
       quant_bounds<LOGN>(H, x[r], ub[r], lb[r]);
     }
@@ -1542,7 +1542,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
         // log2 instead of two, and LGMM's log x cancels; the exponents are
         // integers (exact difference), a NaN / -inf lpdf gives a NaN score
         sc = (b.x == -INFINITY || a.x == -INFINITY) ? NAN
-                                                    : ((b.x - a.x) + log2(b.y / a.y)) * LN2;
+                                                    : ((b.x - a.x) + fast_log2(b.y / a.y)) * LN2;
       }
     } else if constexpr (ERF) {
       lpb = log(sm.merged[0][r][lane].x) - ib.log_pacc;
