@@ -146,6 +146,7 @@ struct tpe_plan {
   StepKey graph_key, pending_key;
   bool graph_ok = false, pending = false;
   bool capturing = false;  // enqueue_step under graph capture (no per-call patch of score seeds)
+  bool mom_fresh = false;  // the last fit wrote the moment table (fit_args)
   hipGraph_t graph = nullptr;
   hipGraphExec_t graph_exec = nullptr;
   std::vector<hipGraphNode_t> fit_nodes, draw_nodes;
@@ -582,11 +583,14 @@ ScoreArgs base_args(tpe_plan *p, int64_t n_sug) {
   a.n_suggest = (int32_t)n_sug;
   a.lat_info = p->d_lat_info;
   a.lat = p->d_lat;
-  a.lse_mom = moment_on() ? 1 : 0;
+  a.lse_mom = moment_on() && p->mom_fresh ? 1 : 0;
   return a;
 }
 
-FitArgs fit_args(tpe_plan *p, int32_t n_below, double prior_weight, int32_t lf) {
+// mom: write the moment table (CoefM) -- only the wave tiles of sorted draws
+// read it; plan.mom_fresh records whether the tables hold it
+FitArgs fit_args(tpe_plan *p, int32_t n_below, double prior_weight, int32_t lf, bool mom = true) {
+  p->mom_fresh = mom;
   FitArgs a{};
   a.hps = p->d_hps;
   a.vals = p->d_vals;
@@ -604,7 +608,7 @@ FitArgs fit_args(tpe_plan *p, int32_t n_below, double prior_weight, int32_t lf) 
   a.info = p->d_info;
   a.coef = p->d_coef;
   a.coef32 = p->d_coef32;
-  a.coefm = p->d_coefm;
+  a.coefm = mom ? p->d_coefm : nullptr;
   a.kcap = p->kcap;
   a.ob = p->d_scratch;
   a.tmp = p->d_scratch;
@@ -1450,7 +1454,17 @@ namespace {
 // enqueue fit + every level's suggest on st (eager or under capture)
 int enqueue_step(tpe_engine *h, tpe_plan *p, int32_t nb, double prior_weight, int32_t lf,
                  int64_t n_sug, int64_t n_cand, hipStream_t st) {
-  CKH(launch_fit(fit_args(p, nb, prior_weight, lf), p->P, st));
+  // the moment table only for a step whose suggest takes a sorted draw
+  // (run_level's sorted_draw: n_cand x n_sug x level hps >= 2^22) on
+  // two-row wave tiles; the others skip its ~3-5 us in k_fit
+  // -- and two-row wave tiles: the one-row tiles of <= kWaveRowSplitMax
+  // candidates find few chunks narrow enough (config 3: 5 % of its pairs)
+  bool mom = n_cand > kWaveRowSplitMax;
+  bool sorted = false;
+  for (const auto &l : p->levels)
+    sorted |= n_cand * n_sug * (int64_t)l.size() >= ((int64_t)1 << 22);
+  mom = mom && sorted;
+  CKH(launch_fit(fit_args(p, nb, prior_weight, lf, mom && moment_on()), p->P, st));
   p->last_nb = nb;
   for (int l = 0; l < (int)p->levels.size(); ++l) {
     const int rc = run_level(h, p, l, n_sug, n_cand, 0, n_cand, st);

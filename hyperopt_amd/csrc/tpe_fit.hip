@@ -817,7 +817,8 @@ __device__ __forceinline__ void store_table(const tpe_hp &H, Coef *cf, Coef32 *c
   // components are active together for the shuffles; kp16 (log-sum-exp):
   // the 16 lanes of a moment chunk likewise (lanes past kp are padding of
   // the chunk only, with no coefficient entry)
-  for (int k = threadIdx.x; k < (quant ? K : kp16); k += blockDim.x) {
+  // (cfm null: the moment table is not wanted by this fit's suggest)
+  for (int k = threadIdx.x; k < (quant ? K : cfm ? kp16 : kp); k += blockDim.x) {
     EnvTerm e{0.0, 0.0, 0.0};
     const bool real = k < K;
     const Coef c = real ? make_coef(H, w[k], mu[k], sg[k], pacc, &e)
@@ -826,7 +827,7 @@ __device__ __forceinline__ void store_table(const tpe_hp &H, Coef *cf, Coef32 *c
       store_coef(cf, k, c, quant);
       if (!quant) store_lse_envelope(cf, k, e, real, c, cf32);
     }
-    if (!quant) store_lse_moments(cfm, k, e, real);
+    if (!quant && cfm) store_lse_moments(cfm, k, e, real);
   }
 }
 
@@ -970,7 +971,7 @@ __device__ __forceinline__ void fit_continuous(const FitArgs &A, const FitCtx &C
   const bool quant = (H.flags & TPE_HAS_Q) != 0;
   Coef *cf = A.coef + slot * A.kcap;
   Coef32 *cf32 = A.coef32 + slot * (A.kcap / kCoefBlock);
-  CoefM *cfm = A.coefm + slot * mom_stride(A.kcap);
+  CoefM *cfm = A.coefm ? A.coefm + slot * mom_stride(A.kcap) : nullptr;
   if (MIXLDS)
     for (int k = threadIdx.x; k < K; k += blockDim.x) { gw[k] = w[k]; gm[k] = mu[k]; gs[k] = sg[k]; }
   store_table(H, cf, cf32, cfm, K, w, mu, sg, pacc, quant);
