@@ -42,6 +42,15 @@ static bool lookup_fork_on() {
   }();
   return on;
 }
+// TPE_PUBLISH=0: results to the host by a runtime copy + stream synchronize
+// instead of k_publish + a spin on its completion word
+static bool publish_on() {
+  static const bool on = [] {
+    const char *e = std::getenv("TPE_PUBLISH");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
 static bool side_streams_on() {
   static const bool on = std::getenv("TPE_SIDE_STREAMS") != nullptr;
   return on;
@@ -90,6 +99,8 @@ struct tpe_plan {
   Partial *d_results = nullptr;
   tpe_result *h_results = nullptr;  // pinned host staging of the results copy
   size_t h_results_cap = 0;
+  uint64_t *h_flag = nullptr;       // pinned completion word of k_publish
+  uint64_t seq = 0;
   uint64_t *d_seeds = nullptr;
   Partial *d_partial = nullptr;
   size_t partial_cap = 0;
@@ -208,6 +219,8 @@ void plan_free_buffers(tpe_plan *p) {
   if (p->h_results) (void)hipHostFree(p->h_results);
   p->h_results = nullptr;
   p->h_results_cap = 0;
+  if (p->h_flag) (void)hipHostFree(p->h_flag);
+  p->h_flag = nullptr;
   if (p->ev0) (void)hipEventDestroy(p->ev0);
   if (p->ev1) (void)hipEventDestroy(p->ev1);
   if (p->ev_fork) (void)hipEventDestroy(p->ev_fork);
@@ -964,16 +977,41 @@ int copy_results(tpe_engine *h, tpe_plan *p, int64_t n_sug, tpe_result *out, int
   // to the host through a pinned staging buffer of the plan: a DMA copy
   // without the runtime's pageable-memory staging (a few hundred bytes; the
   // copy's latency is most of what the caller waits for after the kernels)
+  // (fine-grained coherent pinned memory: the kernel's stores reach it
+  // directly and the host reads them without a runtime copy)
   if (bytes > p->h_results_cap) {
     if (p->h_results) (void)hipHostFree(p->h_results);
     p->h_results = nullptr;
     p->h_results_cap = 0;
     const size_t cap = std::max<size_t>(bytes, 4096);
-    CKH(hipHostMalloc((void **)&p->h_results, cap, hipHostMallocDefault));
+    CKH(hipHostMalloc((void **)&p->h_results, cap, hipHostMallocCoherent | hipHostMallocMapped));
     p->h_results_cap = cap;
   }
-  CKH(hipMemcpyAsync(p->h_results, p->d_results, bytes, hipMemcpyDeviceToHost, st));
-  CKH(hipStreamSynchronize(st));  // (a hipStreamQuery spin measured 2-3 us slower)
+  if (!publish_on()) {
+    CKH(hipMemcpyAsync(p->h_results, p->d_results, bytes, hipMemcpyDeviceToHost, st));
+    CKH(hipStreamSynchronize(st));
+    std::memcpy(out, p->h_results, bytes);
+    return TPE_OK;
+  }
+  if (!p->h_flag) {
+    CKH(hipHostMalloc((void **)&p->h_flag, 64, hipHostMallocCoherent | hipHostMallocMapped));
+    __atomic_store_n(p->h_flag, (uint64_t)0, __ATOMIC_RELEASE);
+  }
+  const uint64_t seq = ++p->seq;
+  CKH(launch_publish(p->d_results, p->h_results, bytes, p->h_flag, seq, st));
+  // spin on the completion word (a stream synchronize's wake-up is the
+  // larger part of a small suggest's host-side wait); every 2^12 polls the
+  // stream is asked for an error, so a failed launch cannot spin forever
+  for (uint64_t it = 1;; ++it) {
+    if (__atomic_load_n(p->h_flag, __ATOMIC_ACQUIRE) == seq) break;
+    __builtin_ia32_pause();
+    if ((it & 4095) == 0) {
+      const hipError_t q = hipStreamQuery(st);
+      if (q != hipSuccess && q != hipErrorNotReady) return fail(h, TPE_E_HIP, hipGetErrorString(q));
+      if (q == hipSuccess && __atomic_load_n(p->h_flag, __ATOMIC_ACQUIRE) != seq)
+        return fail(h, TPE_E_HIP, "k_publish finished without its completion word");
+    }
+  }
   std::memcpy(out, p->h_results, bytes);
   return TPE_OK;
 }

@@ -379,6 +379,10 @@ hipError_t launch_sort_ext(const ScoreArgs &a, const double *src, int32_t *pos_o
                            hipStream_t st);
 // slots slot_begin .. n_slots-1 (the lattice slots before them are not bucketed)
 hipError_t launch_bucket(const ScoreArgs &a, int32_t slot_begin, int32_t *pos_out, hipStream_t st);
+// copy `bytes` (a multiple of 8) to the pinned host buffer dst, then store
+// seq to the pinned word *flag (k_publish)
+hipError_t launch_publish(const void *src, void *dst, size_t bytes, uint64_t *flag, uint64_t seq,
+                          hipStream_t st);
 hipError_t launch_merge(const int32_t *level_hps, int32_t n_slots,
                         int32_t n_suggest, int32_t n_hp, int32_t world,
                         const Partial *gathered, Partial *results,

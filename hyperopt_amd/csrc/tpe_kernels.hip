@@ -659,6 +659,30 @@ hipError_t launch_bucket(const ScoreArgs &a, int32_t slot_begin, int32_t *pos_ou
   return hipGetLastError();
 }
 
+// The suggest's records straight into the caller's pinned host buffer
+// (fine-grained, coherent) and then a sequence number beside them: the host
+// spins on that word instead of a runtime copy + stream synchronize (the
+// latency a caller of one small suggest waits for after the kernels).  The
+// record stores complete before the flag (a system-scope release), every
+// store is a vector store.
+__global__ __launch_bounds__(256) void k_publish(const uint64_t *__restrict__ src,
+                                                 uint64_t *__restrict__ dst, int64_t n_words,
+                                                 uint64_t *__restrict__ flag, uint64_t seq) {
+  for (int64_t i = threadIdx.x; i < n_words; i += blockDim.x) dst[i] = src[i];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+hipError_t launch_publish(const void *src, void *dst, size_t bytes, uint64_t *flag, uint64_t seq,
+                          hipStream_t st) {
+  k_publish<<<1, 256, 0, st>>>(static_cast<const uint64_t *>(src), static_cast<uint64_t *>(dst),
+                               (int64_t)(bytes / 8), flag, seq);
+  return hipGetLastError();
+}
+
 hipError_t launch_merge(const int32_t *level_hps, int32_t n_slots, int32_t n_suggest,
                         int32_t n_hp, int32_t world, const Partial *gathered,
                         Partial *results, hipStream_t st) {
