@@ -605,13 +605,21 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
   const int nch = (nb + kChunk - 1) / kChunk;
   const double *tb = reinterpret_cast<const double *>(cv);
   // pass 1: the largest live block bound of the wave's chunks, and the block
+  // (and the first and last round with a live block: pass 2, whose
+  // threshold is only ever tightened, has no live block outside them)
   float bmax = -INFINITY;
-  int barg = -1;
+  int barg = -1, rf = -1, rl = -1;
   for (int r0 = c0; r0 < nch; r0 += STRIDE * 32) {
     const int k0 = round_k<STRIDE>(r0, lane);
+    bool lv = false;
     if (r0 + STRIDE * (lane >> 1) < nch && k0 < nb) {
       const float b = envelope_bound(block_env<STG>(tb, stg, k0), win);
-      if (b >= win.thr && b > bmax) { bmax = b; barg = k0; }
+      lv = b >= win.thr;
+      if (lv && b > bmax) { bmax = b; barg = k0; }
+    }
+    if (__ballot(lv)) {
+      rf = rf < 0 ? r0 : rf;
+      rl = r0;
     }
   }
   float wmax = bmax;
@@ -659,7 +667,10 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
     WINFO(1, 1);
 #pragma unroll
     for (int r = 0; r < KR; ++r) s[r] = 0.0;
-    for (int r0 = c0; r0 < nch; r0 += STRIDE * 32) {
+    // the rounds pass 1 found live (every round in census builds, whose
+    // totals count the skipped blocks too)
+    const int rb = CENSUS ? c0 : rf, re = CENSUS ? nch : rl + 1;
+    for (int r0 = rb; r0 < re; r0 += STRIDE * 32) {
       const int k0 = round_k<STRIDE>(r0, lane);
       const bool has = r0 + STRIDE * (lane >> 1) < nch && k0 < nb;
       bool live = false, wide = false;
