@@ -1399,7 +1399,7 @@ int tpe_plan_fit(tpe_plan_t p, double gamma, int32_t gamma_cap, double prior_wei
   hipStream_t st = pick_stream(h, stream);
   const double nbf = std::ceil(gamma * std::sqrt((double)p->n));
   const int32_t nb = (int32_t)std::max(0.0, std::min<double>(nbf, gamma_cap));
-  CKH(launch_fit(fit_args(p, nb, prior_weight, lf), p->P, st));
+  CKH(launch_fit(fit_args(p, nb, prior_weight, lf, moment_on()), p->P, st));
   p->last_nb = nb;
   return TPE_OK;
 }
