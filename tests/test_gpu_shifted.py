@@ -543,6 +543,38 @@ print('hex', res.view(np.uint8).tobytes().hex())
     assert a.split('hex ')[1].strip() == b.split('hex ')[1].strip()
 
 
+@pytest.mark.parametrize('env', [{'TPE_LOOKUP_DRAW': '0'}, {'TPE_LOOKUP_FORK': '0'},
+                                 {'TPE_SIDE_STREAMS': '1'}, {'TPE_PUBLISH': '0'}],
+                         ids=['lookup_from_draw', 'lookup_in_order', 'side_streams', 'no_publish'])
+def test_launch_switches_identical_results(env):
+    """The launch-shape switches change no result: lookup slots written by
+    the sorted draw instead of drawn in their tiles (TPE_LOOKUP_DRAW=0), the
+    lookup launch in order instead of forked (TPE_LOOKUP_FORK=0), the forked
+    lattice / mixed-level launches (TPE_SIDE_STREAMS=1) and the runtime copy
+    of the results (TPE_PUBLISH=0) -- a config-3 suggest of 1e5 candidates
+    (two levels, lattice and categorical lookups beside log-sum-exp slots)
+    and a batched config-2 suggest of 3e5, byte-identical to the defaults."""
+    code = """
+import sys, numpy as np
+sys.path.insert(0, 'tests')
+import bench
+from hyperopt_amd import _engine as E
+out = []
+for cfg, seeds, n in (('cfg3', [31337], 100000), ('cfg2', [5, 6, 7], 300000)):
+    dom, losses, vals, act = bench.build_workload(cfg)
+    hps, conds, pprior = dom.space.engine_tables()
+    plan = E.Plan(E.default_engine(), hps, conds, pprior, max_trials=losses.size)
+    plan.set_history(losses, vals, act)
+    res = plan.fit_suggest(seeds, n)
+    assert (res['index'][res['active'] != 0] >= 0).all()
+    out.append(res.view(np.uint8).tobytes().hex())
+print('hex', ':'.join(out))
+"""
+    a = _child(code, env)
+    b = _child(code, {})
+    assert a.split('hex ')[1].strip() == b.split('hex ')[1].strip()
+
+
 def test_sorted_wave_tiles_argmax_numpy_semantics():
     """The production large-draw form (value-bucketed blocks, wave tiles,
     prune mode 3) returns numpy's argmax of its own lpdf difference
