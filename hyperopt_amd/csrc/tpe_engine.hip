@@ -730,12 +730,37 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
   // 0.201 ms forked (the cross-stream joins cost more than the overlap saves;
   // configs 2 and 5 unchanged, profiles/rd5h_*)
   const bool lat_side = lat_level && !fuse_draw && side_streams_on();
-  if (lat_level && !fuse_draw) {
-    ScoreArgs la = base_args(p, n_sug);
-    la.level_hps = lvl;
-    la.n_slots = n_level;
-    la.slot_rows = slot_rows;
-    la.compact = compact ? 1 : 0;
+  // the lattice's readers are the lookup tiles: when those are forked beside
+  // a sorted draw (below), the lattice goes first on the same auxiliary
+  // stream -- in order before its readers, beside the draw and the
+  // log-sum-exp scoring, one join after them (lat_defer; no fork of its own)
+  bool has_other = false;
+  for (int i = 0; i < n_level; ++i) has_other |= !(kinds[i] == KIND_LAT || kinds[i] == KIND_CAT);
+  const bool sorted0 = !fuse_draw && table_draw &&
+                       std::min(chunk, n_cand) * n_sug * n_level >= ((int64_t)1 << 22);
+  const bool lk_inline = sorted0 && kmax <= kFuseTab && !p->capturing && lookup_draw_on();
+  const bool lat_defer = lat_level && !fuse_draw && !lat_side && has_other && lk_inline &&
+                         lookup_fork_on();
+  ScoreArgs la = base_args(p, n_sug);
+  la.level_hps = lvl;
+  la.n_slots = n_level;
+  la.slot_rows = slot_rows;
+  la.compact = compact ? 1 : 0;
+  auto lattice = [&](hipStream_t sl) -> int {
+    tpe_plan::Prof *pr = nullptr;
+    if (p->prof_cap > 0 && p->prof[1].n < p->prof_cap) pr = &p->prof[1];
+    if (pr) CKH(hipEventRecord(pr->a[pr->n], sl));
+    CKH(launch_lattice(la, p->levels[level].data(), p->hps.data(), p->lat.data(), n_lat,
+                       p->d_lat, sl, lat_rows));
+    if (pr) {
+      CKH(hipEventRecord(pr->b[pr->n], sl));
+      pr->pairs[pr->n] = (double)level;
+      pr->n++;
+    }
+    return TPE_OK;
+  };
+  bool lat_pending = lat_defer;
+  if (lat_level && !fuse_draw && !lat_defer) {
     hipStream_t sl = st;
     if (lat_side) {
       sl = h->aux[0];
@@ -745,20 +770,7 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
     // everything after the fork: a failure still records the join event on
     // the side stream and waits on it from st, so a captured graph is never
     // left forked (the chunk loop below joins on its own exits likewise)
-    auto lattice = [&]() -> int {
-      tpe_plan::Prof *pr = nullptr;
-      if (p->prof_cap > 0 && p->prof[1].n < p->prof_cap) pr = &p->prof[1];
-      if (pr) CKH(hipEventRecord(pr->a[pr->n], sl));
-      CKH(launch_lattice(la, p->levels[level].data(), p->hps.data(), p->lat.data(), n_lat,
-                         p->d_lat, sl, lat_rows));
-      if (pr) {
-        CKH(hipEventRecord(pr->b[pr->n], sl));
-        pr->pairs[pr->n] = (double)level;
-        pr->n++;
-      }
-      return TPE_OK;
-    };
-    const int lrc = lattice();
+    const int lrc = lattice(sl);
     if (lat_side) {
       const hipError_t e1 = hipEventRecord(p->ev_join[0], sl);
       if (lrc) {
@@ -859,7 +871,9 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
     // lookup slots drawn by their scoring tiles (no write / read-back of their
     // candidates); not in a captured graph, whose replays patch the seeds of
     // the draw nodes only
-    a.lookup_draw = sorted_draw && !p->capturing && lookup_draw_on() ? 1 : 0;
+    // (every lookup slot's below mixture within the tile's LDS table, so all
+    // of them are drawn in their tiles and none reads the draw's output)
+    a.lookup_draw = sorted_draw && kmax <= kFuseTab && !p->capturing && lookup_draw_on() ? 1 : 0;
     a.lse_prune = (sorted_draw || small_sort) ? p->prune_mode : 0;
     a.lse_shift_min = lse_shift_min();
     // prune mode 3's block-local fp32 pairs on every log-sum-exp slot of the
@@ -875,12 +889,23 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
     if (lk_fork) {
       CKH(hipEventRecord(p->ev_join[3], st));
       CKH(hipStreamWaitEvent(h->aux[2], p->ev_join[3], 0));
-      const hipError_t el = launch_score(a, erf_level, h->aux[2], nullptr, nullptr, nullptr, 2);
+      int lrc = TPE_OK;
+      if (lat_pending) {  // the deferred lattice, ahead of its readers
+        lrc = lattice(h->aux[2]);
+        lat_pending = false;
+      }
+      const hipError_t el = lrc ? hipErrorUnknown
+                                : launch_score(a, erf_level, h->aux[2], nullptr, nullptr, nullptr, 2);
       CKH(hipEventRecord(p->ev_join[4], h->aux[2]));
       if (el != hipSuccess) {
         (void)hipStreamWaitEvent(st, p->ev_join[4], 0);
         return fail(h, TPE_E_HIP, "lookup launch");
       }
+    }
+    if (lat_pending) {  // (no lookup fork after all: the lattice in order)
+      lat_pending = false;
+      const int lrc = lattice(st);
+      if (lrc) return lrc;
     }
     // (every exit below joins the lookup stream back first)
     auto join_lk = [&]() {

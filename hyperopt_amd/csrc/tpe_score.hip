@@ -909,7 +909,14 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
     if (__all(ok)) break;
     if (attempt > 0 || !__all(ok || smax >= 0x1p-100)) return false;
     // lanes that fit keep M (identical second pass); the others re-centre
-    if (!ok) M += ceil(log2(smax)) + 1.0;
+    // ceil(log2 smax) from the exponent of smax = m 2^e (m in [1/2, 1)): e,
+    // or e - 1 when smax is a power of two -- exactly the library's value,
+    // without its polynomial constants held in (spilled) registers
+    if (!ok) {
+      const int e = __builtin_amdgcn_frexp_exp(smax);
+      const double mt = __builtin_amdgcn_frexp_mant(smax);
+      M += (double)(mt == 0.5 ? e - 1 : e) + 1.0;
+    }
   }
 #pragma unroll
   for (int r = 0; r < KR; ++r) out[r] = (y[r] != y[r]) ? LseAcc{NAN, NAN} : LseAcc{M, s[r]};
