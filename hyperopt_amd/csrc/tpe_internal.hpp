@@ -275,6 +275,7 @@ struct ScoreArgs {
   int32_t lookup_draw;       // the sorted draw leaves the lookup slots (categorical, value
                              // lattice) unwritten and the scoring tile draws them itself,
                              // for below mixtures of 1 .. kFuseTab components (lookup_inline)
+  int64_t lookup_seg;        // candidates per lookup-scan block (set by the lookup launch)
   const LatInfo *lat_info;   // [P] value lattices (KIND_LAT slots)
   const double2 *lat;        // lattice (lpdf below, lpdf above) pairs
 };

@@ -1154,6 +1154,10 @@ struct ScoreSmemT {
 #endif
   uint32_t arrive;                      // wave tiles: waves done with the tile
   DrawTableT<kFuseTab> dt;              // lookup tiles drawing their candidates (lookup_inline)
+  double top_s;                         // lookup scans: the best score any value can get
+  int top_nan;                          //   (a NaN score: top is NaN)
+  double red_s[kWaves];                 //   its per-wave partial maxima
+  int red_n[kWaves];
 };
 typedef ScoreSmemT<kRMax> ScoreSmem;
 // k_score_wave1: one candidate row, and the staged tables beside it
@@ -1251,6 +1255,47 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
   if constexpr (LDRAW && (LAT || KIND == KIND_CAT)) {
     ldraw = lookup_inline(A, ib.K);  // block-uniform
     if (ldraw) build_table(H, ib.K, A.mw + sb * A.kcap, A.mmu + sb * A.kcap, A.msig + sb * A.kcap, sm.dt);
+    // the scan's early exit (lookup_scan below): the largest score any value
+    // of the slot can take -- over every category (CAT) or lattice point
+    // (LAT), NaN on top as in numpy's argmax
+    double ms = -INFINITY;
+    int mn = 0;
+    if constexpr (LAT) {
+      // (the points a draw can reach: the lattice's two margin points on
+      // each side absorb host/device rounding -- none is reachable for GMM,
+      // whose clamped x / q rounds inside [rint(low / q), rint(high / q)];
+      // for LGMM the device exp may reach one more point on each side)
+      const LatInfo L = A.lat_info[hp];
+      const int64_t m0 = H.family == TPE_LGMM ? 1 : 2;
+      for (int64_t j = m0 + threadIdx.x; j < (int64_t)L.R - m0; j += blockDim.x) {
+        const double2 v = A.lat[L.off + j];
+        const double sc = v.x - v.y;
+        mn |= sc != sc;
+        ms = fmax(ms, sc);
+      }
+    } else {
+      for (int c = threadIdx.x; c < ib.K; c += blockDim.x) {
+        const double sc = reinterpret_cast<const double *>(cb)[coef_off(c, 0)] -
+                          reinterpret_cast<const double *>(ca)[coef_off(c, 0)];
+        mn |= sc != sc;
+        ms = fmax(ms, sc);
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      ms = fmax(ms, __shfl_xor(ms, o, 64));
+      mn |= __shfl_xor(mn, o, 64);
+    }
+    if (lane == 0) { sm.red_s[wave] = ms; sm.red_n[wave] = mn; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double t = -INFINITY;
+      int n = 0;
+      for (int w = 0; w < kWaves; ++w) { t = fmax(t, sm.red_s[w]); n |= sm.red_n[w]; }
+      sm.top_s = t;
+      sm.top_nan = n;
+    }
+    __syncthreads();
   }
   int64_t li[KR];
   bool valid[KR];
@@ -1276,6 +1321,8 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
     li[r] = wt0 + r * 64 + lane;
     valid[r] = li[r] < A.n_cand;
     if constexpr (LDRAW && (LAT || KIND == KIND_CAT)) {
+      x[r] = 0.0;  // (the scan below draws its own)
+      continue;
       if (ldraw) {
         const uint64_t gi = (uint64_t)(A.cand_begin + li[r]);
         const uint64_t seed = suggestion_seed(A, s);
@@ -1513,6 +1560,57 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
 #ifdef TPE_REREAD
   int64_t best_li = -1;  // the bucketed slot of the lane's best (diagnostic build)
 #endif
+  if constexpr (LDRAW && (LAT || KIND == KIND_CAT)) {
+    // Lookup scan (self-drawing lookups): the block owns a segment of
+    // lookup_seg candidates; wave w walks its 256-candidate pieces w, w + 8,
+    // ... in index order, drawing and scoring each candidate, and stops after
+    // the first piece holding a candidate whose score is the slot's top
+    // (top_s / NaN): no later candidate can beat it (numpy's argmax: the
+    // largest score, the first index among equals, NaN first), and the
+    // globally first top candidate lies in some piece t*, which wave t* mod 8
+    // reaches before any piece of its own after it.  The records that result
+    // are the ones the full scan gives.
+    const double top = sm.top_s;
+    const bool tnan = sm.top_nan != 0;
+    const uint64_t seed = suggestion_seed(A, s);
+    const double *mu_b = A.mmu + sb * A.kcap, *sg_b = A.msig + sb * A.kcap;
+    const int64_t seg0 = (int64_t)tile * A.lookup_seg;
+    const int64_t seg1 = min<int64_t>(seg0 + A.lookup_seg, A.n_cand);
+    LatInfo L{};
+    if constexpr (LAT) L = A.lat_info[hp];
+    for (int64_t p0 = seg0 + (int64_t)wave * 64 * KR; p0 < seg1; p0 += (int64_t)kWaves * 64 * KR) {
+      bool hit = false;
+#pragma unroll
+      for (int r = 0; r < KR; ++r) {
+        const int64_t l = p0 + r * 64 + lane;
+        if (l >= seg1) continue;
+        const uint64_t gi = (uint64_t)(A.cand_begin + l);
+        const double xv = draw_table_ool<kFuseTab>(A.hps + hp, ib.K, mu_b, sg_b, &sm.dt,
+                                                   draw_block0(seed, gi, (uint32_t)hp), seed, gi,
+                                                   (uint32_t)hp);
+        double lpb, lpa;
+        if constexpr (LAT) {
+          const double J = rint(xv / H.q);
+          const int64_t idx = fabs(J) < 4.0e15 ? (int64_t)J - L.j0 : -1;
+          const bool in = idx >= 0 && idx < (int64_t)L.R;
+          const double2 v = in ? A.lat[L.off + idx] : make_double2(NAN, NAN);
+          lpb = v.x;
+          lpa = v.y;
+        } else {
+          const int64_t c = (int64_t)xv;
+          const bool in = (xv >= 0.0) && (c < ib.K) && ((double)c == xv);
+          lpb = in ? reinterpret_cast<const double *>(cb)[coef_off(c, 0)] : NAN;
+          lpa = in ? reinterpret_cast<const double *>(ca)[coef_off(c, 0)] : NAN;
+        }
+        const double sc = lpb - lpa;
+        if (A.out_lb) A.out_lb[l] = lpb;
+        if (A.out_la) A.out_la[l] = lpa;
+        hit |= tnan ? (sc != sc) : (sc == top);
+        take_better(best_s, best_v, best_i, sc, xv, (int64_t)gi);
+      }
+      if (__ballot(hit) && !A.out_lb && !A.out_la) break;
+    }
+  } else
 #pragma unroll
   for (int r = 0; r < KR; ++r) {
     if (!valid[r]) continue;
@@ -2163,8 +2261,31 @@ static hipError_t launch_class(const ScoreArgs &a, int cls, bool has_erf, hipStr
     if (a.census) k_score_wave<true><<<g, kWaves * 64, 0, st>>>(a);
     else k_score_wave<false><<<g, kWaves * 64, 0, st>>>(a);
   } else if (cls == 1) {
-    if (a.census) k_score_lookup<true><<<g, kWaves * 64, 0, st>>>(a);
-    else k_score_lookup<false><<<g, kWaves * 64, 0, st>>>(a);
+    // one block per segment of a slot (the scan's early exit works within a
+    // segment) instead of one per 2048-candidate tile: segments of whole
+    // 2048-candidate pieces, as many as keep ~4 blocks per CU busy (a launch
+    // of few rows keeps the tiles' parallelism; config 5's 80 rows per launch
+    // get ~13 segments of ~8e4 candidates per slot)
+    ScoreArgs b = a;
+    int64_t rows_all = 0;
+    for (int i = 0; i < a.n_groups; ++i)
+      rows_all += (a.grp_block0[i + 1] - a.grp_block0[i]) / a.grp_tiles[i];
+    const int64_t pieces = (a.n_cand + 2047) / 2048;
+    const int64_t want = std::max<int64_t>(1, (4 * kNumCUs) / std::max<int64_t>(1, rows_all * a.n_suggest));
+    const int64_t nseg0 = std::min<int64_t>(pieces, want);
+    b.lookup_seg = (pieces + nseg0 - 1) / nseg0 * 2048;
+    const int32_t nseg = (int32_t)((a.n_cand + b.lookup_seg - 1) / b.lookup_seg);
+    int32_t blk = 0;
+    for (int i = 0; i < b.n_groups; ++i) {
+      const int32_t rows = (a.grp_block0[i + 1] - a.grp_block0[i]) / a.grp_tiles[i];
+      b.grp_block0[i] = blk;
+      b.grp_tiles[i] = nseg;
+      blk += rows * nseg;
+    }
+    b.grp_block0[b.n_groups] = blk;
+    const dim3 gl((unsigned)blk, a.n_suggest);
+    if (b.census) k_score_lookup<true><<<gl, kWaves * 64, 0, st>>>(b);
+    else k_score_lookup<false><<<gl, kWaves * 64, 0, st>>>(b);
   } else if (has_erf) {
     if (a.census) k_score<true, true><<<g, kWaves * 64, 0, st>>>(a);
     else k_score<true, false><<<g, kWaves * 64, 0, st>>>(a);
