@@ -51,6 +51,15 @@ static bool publish_on() {
   }();
   return on;
 }
+// TPE_PATCH_DEFER=0: small history updates go out at once (k_hist_patch)
+// instead of riding the next fit's arguments
+static bool patch_defer_on() {
+  static const bool on = [] {
+    const char *e = std::getenv("TPE_PATCH_DEFER");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
 static bool side_streams_on() {
   static const bool on = std::getenv("TPE_SIDE_STREAMS") != nullptr;
   return on;
@@ -158,6 +167,8 @@ struct tpe_plan {
   bool graph_ok = false, pending = false;
   bool capturing = false;  // enqueue_step under graph capture (no per-call patch of score seeds)
   bool mom_fresh = false;  // the last fit wrote the moment table (fit_args)
+  HistPatch pend{};        // a small history update not yet on the device: the next
+  bool has_pend = false;   // fit writes it (k_fit's patch), anything else flushes it
   hipGraph_t graph = nullptr;
   hipGraphExec_t graph_exec = nullptr;
   std::vector<hipGraphNode_t> fit_nodes, draw_nodes;
@@ -628,6 +639,22 @@ FitArgs fit_args(tpe_plan *p, int32_t n_below, double prior_weight, int32_t lf, 
   a.sortbuf = p->d_sortbuf;
   a.scap = p->scap;
   return a;
+}
+
+// a deferred history update onto the device now (k_hist_patch), for every
+// reader other than the fit
+int flush_patch(tpe_engine *h, tpe_plan *p, hipStream_t st) {
+  if (!p->has_pend) return TPE_OK;
+  p->has_pend = false;
+  CKH(launch_hist_patch(p->pend, p->d_vals, p->d_active, p->d_losses, st));
+  return TPE_OK;
+}
+// the fit of a plan, with the deferred history update (if any) written by
+// its blocks first
+int fit_launch(tpe_engine *h, tpe_plan *p, const FitArgs &a, int32_t n_hp, hipStream_t st) {
+  CKH(launch_fit(a, n_hp, st, p->has_pend ? &p->pend : nullptr));
+  p->has_pend = false;
+  return TPE_OK;
 }
 
 int score_launch(tpe_engine *h, tpe_plan *p, ScoreArgs a, bool has_erf, int64_t cn,
@@ -1389,7 +1416,12 @@ int tpe_plan_update_history(tpe_plan_t p, int64_t n, int64_t row0, int64_t n_row
   if (!on_device && n_rows * p->P <= kPatchVals && n_loss <= kPatchLoss) {
     // the fmin steady state (a row or two, a few losses): the values ride in
     // the kernel arguments -- no staging copy, no host synchronisation
-    HistPatch hp{};
+    // -- and deferred: the next fit's blocks write it (one launch less per
+    // fmin step); an earlier one still pending goes out first
+    int rc = flush_patch(h, p, st);
+    if (rc) return rc;
+    HistPatch &hp = p->pend;
+    hp = HistPatch{};
     hp.row0 = row0; hp.n_rows = n_rows; hp.loss0 = loss0; hp.n_loss = n_loss;
     hp.ld = p->ncap; hp.P = p->P;
     for (int i = 0; i < p->P; ++i)
@@ -1398,9 +1430,15 @@ int tpe_plan_update_history(tpe_plan_t p, int64_t n, int64_t row0, int64_t n_row
         hp.active[i * n_rows + r] = active[(int64_t)i * src_ld + r];
       }
     for (int64_t i = 0; i < n_loss; ++i) hp.losses[i] = losses[i];
-    if (n_rows > 0 || n_loss > 0) CKH(launch_hist_patch(hp, p->d_vals, p->d_active, p->d_losses, st));
+    p->has_pend = n_rows > 0 || n_loss > 0;
+    if (p->has_pend && !patch_defer_on()) rc = flush_patch(h, p, st);
+    if (rc) return rc;
     p->n = n;
     return TPE_OK;
+  }
+  {
+    const int rc = flush_patch(h, p, st);
+    if (rc) return rc;
   }
   const hipMemcpyKind kd = on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
   if (n_rows > 0 && p->P > 0) {
@@ -1424,7 +1462,8 @@ int tpe_plan_fit(tpe_plan_t p, double gamma, int32_t gamma_cap, double prior_wei
   hipStream_t st = pick_stream(h, stream);
   const double nbf = std::ceil(gamma * std::sqrt((double)p->n));
   const int32_t nb = (int32_t)std::max(0.0, std::min<double>(nbf, gamma_cap));
-  CKH(launch_fit(fit_args(p, nb, prior_weight, lf, moment_on()), p->P, st));
+  const int rc = fit_launch(h, p, fit_args(p, nb, prior_weight, lf, moment_on()), p->P, st);
+  if (rc) return rc;
   p->last_nb = nb;
   return TPE_OK;
 }
@@ -1527,7 +1566,10 @@ int enqueue_step(tpe_engine *h, tpe_plan *p, int32_t nb, double prior_weight, in
   for (const auto &l : p->levels)
     sorted |= n_cand * n_sug * (int64_t)l.size() >= ((int64_t)1 << 22);
   mom = mom && sorted;
-  CKH(launch_fit(fit_args(p, nb, prior_weight, lf, mom && moment_on()), p->P, st));
+  {
+    const int rc = fit_launch(h, p, fit_args(p, nb, prior_weight, lf, mom && moment_on()), p->P, st);
+    if (rc) return rc;
+  }
   p->last_nb = nb;
   for (int l = 0; l < (int)p->levels.size(); ++l) {
     const int rc = run_level(h, p, l, n_sug, n_cand, 0, n_cand, st);
@@ -1587,7 +1629,8 @@ int launch_step(tpe_engine *h, tpe_plan *p, int32_t nb, const uint64_t *seeds, i
     FitArgs fa = p->fit_args0[i];
     fa.n = p->n;
     fa.n_below = nb;
-    void *args[1] = {&fa};
+    HistPatch none{};  // (the caller flushed any deferred history update)
+    void *args[2] = {&fa, &none};
     hipKernelNodeParams kp = p->fit_params[i];
     kp.kernelParams = args;
     kp.extra = nullptr;
@@ -1649,6 +1692,10 @@ int tpe_plan_fit_suggest(tpe_plan_t p, double gamma, int32_t gamma_cap, double p
   int rc = ensure_suggest_state(h, p, n_sug, 1);
   if (rc) return rc;
   p->h_seeds.assign(seeds, seeds + n_sug);
+  if (graphable) {  // (a graph's fit node carries no history patch)
+    rc = flush_patch(h, p, st);
+    if (rc) return rc;
+  }
   if (!graphable || !((p->graph_ok && p->graph_key == key) || (p->pending && p->pending_key == key))) {
     // eager (first sight of this shape: it also sizes every buffer)
     if (n_sug > kInlineSeeds)

@@ -1147,9 +1147,26 @@ __device__ __forceinline__ void fit_slot(const FitArgs &A, unsigned char *dyn_ld
 // instantiation without the large-history paths keeps the code a CU pair
 // runs (and shares one instruction cache for) small
 template <bool SMALL>
-__global__ __launch_bounds__(kFitThreads) void k_fit(FitArgs A) {
+__global__ __launch_bounds__(kFitThreads) void k_fit(FitArgs A, HistPatch P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn_lds[];
   __shared__ FitShared sm;
+  if (P.n_rows > 0 || P.n_loss > 0) {
+    // the history update that came with this call (tpe_plan_update_history,
+    // deferred into the fit): each block writes its hp's new rows and every
+    // new loss -- the blocks of other hps write the same loss values -- and
+    // reads them back after its own barrier
+    const int hp = blockIdx.x;
+    double *vals = const_cast<double *>(A.vals);
+    uint8_t *act = const_cast<uint8_t *>(A.active);
+    double *losses = const_cast<double *>(A.losses);
+    for (int r = threadIdx.x; r < (int)P.n_rows; r += blockDim.x) {
+      vals[(int64_t)hp * P.ld + P.row0 + r] = P.vals[hp * (int)P.n_rows + r];
+      act[(int64_t)hp * P.ld + P.row0 + r] = P.active[hp * (int)P.n_rows + r];
+    }
+    for (int i = threadIdx.x; i < (int)P.n_loss; i += blockDim.x) losses[P.loss0 + i] = P.losses[i];
+    __threadfence_block();
+    __syncthreads();
+  }
   for (int rep = 0; rep < TPE_FIT_REPS; ++rep) {
     fit_slot<SMALL>(A, dyn_lds, sm);
     __syncthreads();
@@ -1391,10 +1408,12 @@ const void *fit_kernel_fn(bool small) {
                : reinterpret_cast<const void *>(&k_fit<false>);
 }
 
-hipError_t launch_fit(const FitArgs &a, int32_t n_hp, hipStream_t st) {
+hipError_t launch_fit(const FitArgs &a, int32_t n_hp, hipStream_t st, const HistPatch *patch) {
   if (n_hp <= 0) return hipSuccess;
-  if (fit_small(a.n)) k_fit<true><<<dim3(n_hp, 2), kFitThreads, kFitLds, st>>>(a);
-  else k_fit<false><<<dim3(n_hp, 2), kFitThreads, kFitLds, st>>>(a);
+  static const HistPatch none{};
+  const HistPatch &P = patch ? *patch : none;
+  if (fit_small(a.n)) k_fit<true><<<dim3(n_hp, 2), kFitThreads, kFitLds, st>>>(a, P);
+  else k_fit<false><<<dim3(n_hp, 2), kFitThreads, kFitLds, st>>>(a, P);
   return hipGetLastError();
 }
 

@@ -307,7 +307,11 @@ struct FitArgs {
 
 // ---- launch wrappers (tpe_fit.hip / tpe_kernels.hip) ----
 hipError_t launch_split(const FitArgs &a, uint8_t *below, hipStream_t st);
-hipError_t launch_fit(const FitArgs &a, int32_t n_hp, hipStream_t st);
+struct HistPatch;
+// patch: history rows / losses the fit blocks write before they read the
+// history (a deferred tpe_plan_update_history; null: none)
+hipError_t launch_fit(const FitArgs &a, int32_t n_hp, hipStream_t st,
+                      const HistPatch *patch = nullptr);
 bool fit_small(int64_t n);                 // k_fit<true> (all-LDS variant) serves n trials
 const void *fit_kernel_fn(bool small);     // k_fit's host stub (graph node lookup)
 bool is_draw_kernel_fn(const void *f);     // one of k_draw's / k_draw_sorted's host stubs

@@ -527,3 +527,45 @@ def test_small_draw_pruning_in_child_process():
         on, off = np.load(out[0]), np.load(out[1])
     from gpu_util import assert_winners_match
     assert_winners_match(on, off, msg='small-draw pruning')
+
+
+def test_deferred_history_patch_identical():
+    """Small history updates (a few appended trials: tpe_plan_update_history's
+    kernel-argument patch) are deferred into the next fit, whose blocks write
+    them before reading the history; two of them in a row (the first goes out
+    on its own), then fit+suggest, equal a plan given the whole history at
+    once -- byte for byte; a plain fit and a mixture read after a deferred
+    update see it too."""
+    import sys
+    import os
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from hyperopt_amd import _engine as E
+    dom, losses, vals, act = bench.build_workload('cfg2')
+    hps, conds, pprior = dom.space.engine_tables()
+    n = losses.size
+    vals = np.ascontiguousarray(vals, dtype=np.float64)
+    act = np.ascontiguousarray(act, dtype=np.uint8)
+    eng = E.default_engine()
+    full = E.Plan(eng, hps, conds, pprior, max_trials=n)
+    full.set_history(losses, vals, act)
+    ref = full.fit_suggest([11, 12], 4096)
+    part = E.Plan(eng, hps, conds, pprior, max_trials=n)
+    m = n - 3
+    part.set_history(losses[:m], np.ascontiguousarray(vals[:, :m]), np.ascontiguousarray(act[:, :m]))
+    part.fit_suggest([5], 4096)
+    part.update_history(n - 1, m, vals, act, n, m, losses)   # two rows (deferred)
+    part.update_history(n, n - 1, vals, act, n, n - 1, losses)  # one more (the first flushes)
+    got = part.fit_suggest([11, 12], 4096)
+    np.testing.assert_array_equal(got.view(np.uint8), ref.view(np.uint8))
+    # plain fit after a deferred update: the fitted mixtures match
+    part2 = E.Plan(eng, hps, conds, pprior, max_trials=n)
+    part2.set_history(losses[:m], np.ascontiguousarray(vals[:, :m]), np.ascontiguousarray(act[:, :m]))
+    part2.update_history(n, m, vals, act, n, m, losses)
+    part2.fit()
+    full.fit()
+    for h in range(len(hps)):
+        for side in (0, 1):
+            a, b = part2.mixture(h, side), full.mixture(h, side)
+            for x, y in zip(a, b):
+                np.testing.assert_array_equal(x, y)
