@@ -127,14 +127,23 @@ __device__ __forceinline__ void take_better(double &s, double &v, int64_t &i, do
   i = b ? oi : i;
 }
 
+// (the reduction carries (score, index) only; the winner's value comes from
+// the lane that held the winning record -- candidate indices are unique
+// across the lanes, so that lane is the one whose own index won; with no
+// valid record anywhere every lane keeps its own (NaN, NaN, -1))
 __device__ __forceinline__ void wave_best(double &s, double &v, int64_t &i) {
+  const int64_t i0 = i;
+  const double v0 = v;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const double os = __shfl_xor(s, o, 64);
-    const double ov = __shfl_xor(v, o, 64);
     const int64_t oi = __shfl_xor(i, o, 64);
-    take_better(s, v, i, os, ov, oi);
+    const bool b = better(os, oi, s, i);
+    s = b ? os : s;
+    i = b ? oi : i;
   }
+  const uint64_t m = __ballot(i0 == i && i >= 0);
+  v = m ? __shfl(v0, (int)__builtin_ctzll(m), 64) : v0;
 }
 
 // activity of a conditional hp: OR over its (parent active and parent value

@@ -634,20 +634,51 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
     const uint64_t at = __ballot(bmax == wmax && barg >= 0);
     const int kb = __shfl(barg, at ? __builtin_ctzll(at) : 0, 64);
     if (kb >= 0) {
-      CoefGroup g;
-      load_group(cs, __builtin_amdgcn_readfirstlane(kb), g);
+      const int kbu = __builtin_amdgcn_readfirstlane(kb);
       double lo = INFINITY;
+      bool done = false;
+      if constexpr (F32) {
+        // a block that is not wide: its block-local fp32 form, t = A + z
+        // (the maximum term is within ~1 of A, fp32 rounding ~1e-6 on it; a
+        // margin of 1/64 keeps the bound a lower bound)
+        const float4 e = block_env<STG>(tb, stg, kbu);
+        if (!__builtin_signbit(e.w)) {
+          CoefGroup32 g32;
+          if constexpr (STG) load_block32_lds(stg.c32, (unsigned)kbu >> 3, g32);
+          else load_group32(c32, kbu, g32);
+          float lo32 = INFINITY;
 #pragma unroll
-      for (int r = 0; r < KR; ++r) {
-        if (!valid[r]) continue;
-        double mx = -INFINITY;
+          for (int r = 0; r < KR; ++r) {
+            if (!valid[r]) continue;
+            float z[1][kGroup];
+            const double yr[1] = {y[r]};
+            lse_terms_z<1>(g32, yr, z);
+            float mx = z[0][0];
 #pragma unroll
-        for (int j = 0; j < kGroup; ++j)
-          mx = fmax(mx, fma(g.z[j], y[r] * y[r], fma(g.y[j], y[r], g.x[j])));
-        lo = fmin(lo, mx);
+            for (int j = 1; j < kGroup; ++j) mx = fmaxf(mx, z[0][j]);
+            lo32 = fminf(lo32, mx);
+          }
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) lo32 = fminf(lo32, __shfl_xor(lo32, o, 64));
+          lo = (double)g32.A + (double)lo32 - 0.015625;
+          done = true;
+        }
       }
+      if (!done) {
+        CoefGroup g;
+        load_group(cs, kbu, g);
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) lo = fmin(lo, __shfl_xor(lo, o, 64));
+        for (int r = 0; r < KR; ++r) {
+          if (!valid[r]) continue;
+          double mx = -INFINITY;
+#pragma unroll
+          for (int j = 0; j < kGroup; ++j)
+            mx = fmax(mx, fma(g.z[j], y[r] * y[r], fma(g.y[j], y[r], g.x[j])));
+          lo = fmin(lo, mx);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) lo = fmin(lo, __shfl_xor(lo, o, 64));
+      }
       const float dead = kLseDeadBase + (float)(32 - __builtin_clz((unsigned)max(nb - 1, 1)));
       const float t2 = (float)(lo - (double)dead) - 1.0f;
       if (lo > -1.0e30 && lo < 1.0e30 && t2 > win.thr)
