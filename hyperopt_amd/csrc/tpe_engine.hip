@@ -60,6 +60,14 @@ static bool patch_defer_on() {
   }();
   return on;
 }
+// TPE_TILE_DRAW=0: tiny unsorted draws by k_draw instead of their tiles
+static bool tile_draw_on() {
+  static const bool on = [] {
+    const char *e = std::getenv("TPE_TILE_DRAW");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
 static bool side_streams_on() {
   static const bool on = std::getenv("TPE_SIDE_STREAMS") != nullptr;
   return on;
@@ -938,7 +946,15 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
     auto join_lk = [&]() {
       if (lk_fork) (void)hipStreamWaitEvent(st, p->ev_join[4], 0);
     };
-    if (fuse_draw) {
+    // tiny unsorted draws of levels with no lattice and no per-candidate erf
+    // slots: the scoring tiles draw their own candidates (k_score_tdraw) --
+    // one launch less (the config-1 shape: 24 candidates of one hp)
+    const bool tdraw = !sorted_draw && !small_sort && !fuse_draw && !lat_level && !erf_level &&
+                       table_draw && kmax <= kFuseTab && cn <= 4096 && !p->capturing &&
+                       tile_draw_on();
+    a.tile_draw = tdraw ? 1 : 0;
+    if (tdraw) {
+    } else if (fuse_draw) {
       tpe_plan::Prof *pr = nullptr;
       if (p->prof_cap > 0 && p->prof[1].n < p->prof_cap) pr = &p->prof[1];
       if (pr) CKH(hipEventRecord(pr->a[pr->n], st));
@@ -1417,7 +1433,12 @@ int tpe_plan_update_history(tpe_plan_t p, int64_t n, int64_t row0, int64_t n_row
     // the fmin steady state (a row or two, a few losses): the values ride in
     // the kernel arguments -- no staging copy, no host synchronisation
     // -- and deferred: the next fit's blocks write it (one launch less per
-    // fmin step); an earlier one still pending goes out first
+    // fmin step); an earlier one still pending goes out first (an empty
+    // update -- tpe.suggest's own push after the caller's -- keeps it)
+    if (n_rows == 0 && n_loss == 0) {
+      p->n = n;
+      return TPE_OK;
+    }
     int rc = flush_patch(h, p, st);
     if (rc) return rc;
     HistPatch &hp = p->pend;

@@ -276,6 +276,8 @@ struct ScoreArgs {
                              // lattice) unwritten and the scoring tile draws them itself,
                              // for below mixtures of 1 .. kFuseTab components (lookup_inline)
   int64_t lookup_seg;        // candidates per lookup-scan block (set by the lookup launch)
+  int32_t tile_draw;         // tiny unsorted draws: every tile draws its own candidates
+                             // (k_score_tdraw; no k_draw launch, nothing written)
   const LatInfo *lat_info;   // [P] value lattices (KIND_LAT slots)
   const double2 *lat;        // lattice (lpdf below, lpdf above) pairs
 };

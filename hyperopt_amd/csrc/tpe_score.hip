@@ -1216,7 +1216,7 @@ __device__ double g_rr2_ex[64][8];
 
 // (SM: ScoreSmem, or ScoreSmem1 for the one-row wave tiles, whose
 // workgroup stages both mixtures' tables in LDS when they fit kStageBlocks)
-template <int KIND, bool CENSUS, typename SM, bool LDRAW = false>
+template <int KIND, bool CENSUS, typename SM, bool LDRAW = false, bool TDRAW = false>
 __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot, int tile,
                                            int ntiles, bool known_active) {
   constexpr bool STAGE = std::is_same<SM, ScoreSmem1>::value;
@@ -1328,6 +1328,13 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
     }
     __syncthreads();
   }
+  // tiny unsorted draws (ScoreArgs::tile_draw): the tile draws its own
+  // candidates from the below mixture's LDS table -- the table and values of
+  // k_draw<true> (K <= kFuseTab: the host only takes this path then)
+  if constexpr (TDRAW) {
+    if (ib.K >= 1 && ib.K <= kFuseTab)
+      build_table(H, ib.K, A.mw + sb * A.kcap, A.mmu + sb * A.kcap, A.msig + sb * A.kcap, sm.dt);
+  }
   int64_t li[KR];
   bool valid[KR];
   double x[KR], y[KR], ub[KR], lb[KR];
@@ -1367,6 +1374,17 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
       } else {
         x[r] = valid[r] ? cand[li[r]] : 0.0;
       }
+    } else if constexpr (TDRAW) {
+      const uint64_t gi = (uint64_t)(A.cand_begin + li[r]);
+      const uint64_t seed = suggestion_seed(A, s);
+      const bool tab = ib.K >= 1 && ib.K <= kFuseTab;
+      x[r] = !valid[r] ? (LOGN ? 1.0 : 0.0)
+             : tab ? draw_table_ool<kFuseTab>(A.hps + hp, ib.K, A.mmu + sb * A.kcap,
+                                              A.msig + sb * A.kcap, &sm.dt,
+                                              draw_block0(seed, gi, (uint32_t)hp), seed, gi,
+                                              (uint32_t)hp)
+                   : draw_one_ool(A.hps + hp, A.info + sb, A.mw + sb * A.kcap, A.mmu + sb * A.kcap,
+                                  A.msig + sb * A.kcap, seed, gi, (uint32_t)hp);
     } else {
       x[r] = valid[r] ? cand[li[r]] : (LOGN ? 1.0 : 0.0);
     }
@@ -1957,7 +1975,7 @@ __device__ __forceinline__ void mark_inactive(const ScoreArgs &A, int s, int s0,
 // erf ones, every kind, or only the wave-tile log-sum-exp kinds (levels of
 // large draws whose every slot is one: a kernel with only their register
 // allocation -- the combined one keeps the most any kind needs).
-enum { kSetNoErf = 0, kSetAll = 1, kSetWave = 2, kSetWave1 = 3, kSetLookup = 4 };
+enum { kSetNoErf = 0, kSetAll = 1, kSetWave = 2, kSetWave1 = 3, kSetLookup = 4, kSetTiny = 5 };
 
 template <int SET, bool CENSUS, typename SM>
 __device__ __forceinline__ void score_block(const ScoreArgs &A, SM &sm) {
@@ -1983,6 +2001,17 @@ __device__ __forceinline__ void score_block(const ScoreArgs &A, SM &sm) {
   } else if constexpr (SET == kSetLookup) {
     if (A.grp_kind[g] == KIND_LAT) score_tile<KIND_LAT, CENSUS, SM, true>(A, sm, slot, tile, nt, known);
     else score_tile<KIND_CAT, CENSUS, SM, true>(A, sm, slot, tile, nt, known);
+    return;
+  } else if constexpr (SET == kSetTiny) {
+    // (tiny unsorted draws of levels without lattice or per-candidate erf
+    // slots: the log-sum-exp kinds and categoricals, each tile drawing)
+    switch (A.grp_kind[g]) {
+      case KIND_LSE_G: score_tile<KIND_LSE_G, CENSUS, SM, false, true>(A, sm, slot, tile, nt, known); break;
+      case KIND_LSE_L: score_tile<KIND_LSE_L, CENSUS, SM, false, true>(A, sm, slot, tile, nt, known); break;
+      case KIND_LSE_G1: score_tile<KIND_LSE_G1, CENSUS, SM, false, true>(A, sm, slot, tile, nt, known); break;
+      case KIND_LSE_L1: score_tile<KIND_LSE_L1, CENSUS, SM, false, true>(A, sm, slot, tile, nt, known); break;
+      default: score_tile<KIND_CAT, CENSUS, SM, false, true>(A, sm, slot, tile, nt, known); break;
+    }
     return;
   } else if constexpr (SET == kSetWave1) {
     if (A.grp_kind[g] == KIND_LSE_LW1) score_tile<KIND_LSE_LW1, CENSUS, SM>(A, sm, slot, tile, nt, known);
@@ -2031,6 +2060,15 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(TPE
 void k_score_wave1(ScoreArgs A) {
   __shared__ ScoreSmem1 sm;
   score_block<kSetWave1, CENSUS>(A, sm);
+}
+
+// tiny unsorted draws whose tiles draw their own candidates (tile_draw), in a
+// kernel of their own (the draw's call out of k_score's register allocation)
+template <bool CENSUS>
+__global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(4)))
+void k_score_tdraw(ScoreArgs A) {
+  __shared__ ScoreSmem sm;
+  score_block<kSetTiny, CENSUS>(A, sm);
 }
 
 // the lookup tiles (categorical, value lattice) that draw their own
@@ -2337,6 +2375,12 @@ hipError_t launch_score(const ScoreArgs &a, bool has_erf, hipStream_t st, hipStr
                         hipEvent_t ev_fork, hipEvent_t ev_join, int classes) {
   if (a.n_groups <= 0 || a.n_suggest <= 0) return hipSuccess;
   if (a.grp_block0[a.n_groups] <= 0) return hipSuccess;
+  if (a.tile_draw) {  // (every group: the host takes this path for such levels only)
+    const dim3 g((unsigned)a.grp_block0[a.n_groups], a.n_suggest);
+    if (a.census) k_score_tdraw<true><<<g, kWaves * 64, 0, st>>>(a);
+    else k_score_tdraw<false><<<g, kWaves * 64, 0, st>>>(a);
+    return hipGetLastError();
+  }
   bool has[3] = {false, false, false};
   for (int i = 0; i < a.n_groups; ++i) has[group_class(a, a.grp_kind[i])] = true;
   for (int c = 0; c < 3; ++c) has[c] = has[c] && ((classes >> c) & 1);
