@@ -963,27 +963,30 @@ struct LseRange {
 };
 template <int KR>
 __device__ __forceinline__ LseRange lse_range(const double (&y)[KR], const bool (&valid)[KR]) {
-  double lo = INFINITY, hi = -INFINITY;
+  // (each lane rounds its own values outward to fp32 and the wave reduces
+  // those: rounding is monotone, so this is the fp32-outward rounding of the
+  // fp64 extremes -- the same floats as reducing in fp64, half the shuffles)
+  float wl = INFINITY, wh = -INFINITY;
   bool ok = true;
 #pragma unroll
   for (int r = 0; r < KR; ++r) {
     if (!valid[r]) continue;
     ok &= fabs(y[r]) < INFINITY;
-    lo = fmin(lo, y[r]);
-    hi = fmax(hi, y[r]);
+    const float f = (float)y[r];
+    const float fl = ((double)f > y[r]) ? nextafterf(f, -INFINITY) : f;
+    const float fh = ((double)f < y[r]) ? nextafterf(f, INFINITY) : f;
+    wl = fminf(wl, fl);
+    wh = fmaxf(wh, fh);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
-    lo = fmin(lo, __shfl_xor(lo, o, 64));
-    hi = fmax(hi, __shfl_xor(hi, o, 64));
+    wl = fminf(wl, __shfl_xor(wl, o, 64));
+    wh = fmaxf(wh, __shfl_xor(wh, o, 64));
   }
-  const float flo = (float)lo, fhi = (float)hi;
-  const float wl = ((double)flo > lo) ? nextafterf(flo, -INFINITY) : flo;
-  const float wh = ((double)fhi < hi) ? nextafterf(fhi, INFINITY) : fhi;
   auto sf = [](float v) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
   };
-  return LseRange{sf(wl), sf(wh), __all(ok) != 0, lo <= hi};
+  return LseRange{sf(wl), sf(wh), __all(ok) != 0, wl <= wh};
 }
 
 // PRUNE setup, part 2 (per mixture): from the mixture's probe component (its
@@ -1001,12 +1004,17 @@ __device__ __forceinline__ LseWindow lse_window(KDbl *__restrict__ cs, int probe
 #pragma unroll
   for (int r = 0; r < KR; ++r)
     if (valid[r]) tmin = fmin(tmin, fma(fma(pz, y[r], py), y[r], px));
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) tmin = fmin(tmin, __shfl_xor(tmin, o, 64));
-  ok = ok && tmin == tmin && tmin > -1.0e30;
-  // threshold one unit conservative; the (wave-uniform) values travel in SGPRs
+  // threshold one unit conservative; the (wave-uniform) values travel in SGPRs.
+  // Each lane maps its own minimum through the (monotone) fp32 threshold and
+  // the wave takes the smallest: the threshold of the wave's minimum, with
+  // one fp32 reduction instead of an fp64 one (fmin never yields NaN here:
+  // it starts at +inf and skips NaN terms); the validity test by ballot
   const float dead = kLseDeadBase + (float)(32 - __builtin_clz((unsigned)max(K - 1, 1)));
-  float th = ok ? (float)(tmin - (double)dead) - 1.0f : -INFINITY;
+  float thl = (float)(tmin - (double)dead) - 1.0f;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) thl = fminf(thl, __shfl_xor(thl, o, 64));
+  ok = ok && __all(tmin > -1.0e30);
+  float th = ok ? thl : -INFINITY;
   if (!rg.any) th = -INFINITY;  // no valid candidate in the wave
   th = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, th)));
   return LseWindow{rg.lo, rg.hi, th};
