@@ -68,6 +68,15 @@ static bool tile_draw_on() {
   }();
   return on;
 }
+// TPE_PUBLISH_FUSE=0: a call whose last launch is a tile_draw scoring launch
+// still ends with k_publish (default: that launch's last record publishes)
+static bool publish_fuse_on() {
+  static const bool on = [] {
+    const char *e = std::getenv("TPE_PUBLISH_FUSE");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
 static bool side_streams_on() {
   static const bool on = std::getenv("TPE_SIDE_STREAMS") != nullptr;
   return on;
@@ -118,6 +127,10 @@ struct tpe_plan {
   size_t h_results_cap = 0;
   uint64_t *h_flag = nullptr;       // pinned completion word of k_publish
   uint64_t seq = 0;
+  // this call's results go to the host and its last launch may publish them
+  // itself (tpe_plan_fit_suggest); pub_fired: it does, with sequence seq
+  bool pub_arm = false;
+  bool pub_fired = false;
   uint64_t *d_seeds = nullptr;
   Partial *d_partial = nullptr;
   size_t partial_cap = 0;
@@ -452,8 +465,9 @@ int ensure_suggest_state(tpe_engine *h, tpe_plan *p, int64_t n_sug, size_t parti
     p->d_ticket = nullptr;
     CKH(dalloc(&p->d_results, (size_t)n_sug * p->P));
     CKH(dalloc(&p->d_seeds, n_sug));
-    CKH(dalloc(&p->d_ticket, (size_t)n_sug * p->P));
-    CKH(hipMemset(p->d_ticket, 0, (size_t)n_sug * p->P * sizeof(uint32_t)));
+    // (+1: the launch-wide arrival counter of a publishing launch, pub_ticket)
+    CKH(dalloc(&p->d_ticket, (size_t)n_sug * p->P + 1));
+    CKH(hipMemset(p->d_ticket, 0, ((size_t)n_sug * p->P + 1) * sizeof(uint32_t)));
     p->s_cap = n_sug;
   }
   if (partials > p->partial_cap) {
@@ -953,6 +967,19 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
                        table_draw && kmax <= kFuseTab && cn <= 4096 && !p->capturing &&
                        tile_draw_on();
     a.tile_draw = tdraw ? 1 : 0;
+    // the call's last launch (its last level, one chunk, a full grid): its
+    // last final record publishes the call's results (k_publish's work)
+    if (tdraw && p->pub_arm && level + 1 == (int)p->levels.size() && cn == n_cand &&
+        cand_begin == 0 && n_total == n_cand && !compact && !lk_fork && a.n_groups > 0 &&
+        a.grp_block0[a.n_groups] > 0 && publish_fuse_on()) {
+      a.pub_dst = reinterpret_cast<uint64_t *>(p->h_results);
+      a.pub_flag = p->h_flag;
+      a.pub_ticket = p->d_ticket + (size_t)p->s_cap * p->P;
+      a.pub_seq = ++p->seq;
+      a.pub_words = (int32_t)(n_sug * p->P * (int64_t)(sizeof(tpe_result) / 8));
+      a.pub_events = (int32_t)(n_sug * n_level);
+      p->pub_fired = true;
+    }
     if (tdraw) {
     } else if (fuse_draw) {
       tpe_plan::Prof *pr = nullptr;
@@ -1034,8 +1061,11 @@ int run_external(tpe_engine *h, tpe_plan *p, int32_t hp, const double *ext, int6
   return score_launch(h, p, a, kind == KIND_ERF_G || kind == KIND_ERF_L, n, st, false);
 }
 
+int host_results(tpe_engine *h, tpe_plan *p, int64_t n_sug);
+
 int copy_results(tpe_engine *h, tpe_plan *p, int64_t n_sug, tpe_result *out, int32_t on_dev,
                  hipStream_t st) {
+  if (!out || on_dev) p->pub_fired = false;  // (armed for host output only)
   if (!out) return TPE_OK;
   const size_t bytes = (size_t)n_sug * p->P * sizeof(tpe_result);
   if (on_dev) {
@@ -1047,26 +1077,19 @@ int copy_results(tpe_engine *h, tpe_plan *p, int64_t n_sug, tpe_result *out, int
   // copy's latency is most of what the caller waits for after the kernels)
   // (fine-grained coherent pinned memory: the kernel's stores reach it
   // directly and the host reads them without a runtime copy)
-  if (bytes > p->h_results_cap) {
-    if (p->h_results) (void)hipHostFree(p->h_results);
-    p->h_results = nullptr;
-    p->h_results_cap = 0;
-    const size_t cap = std::max<size_t>(bytes, 4096);
-    CKH(hipHostMalloc((void **)&p->h_results, cap, hipHostMallocCoherent | hipHostMallocMapped));
-    p->h_results_cap = cap;
-  }
+  const int rc = host_results(h, p, n_sug);
+  if (rc) return rc;
   if (!publish_on()) {
     CKH(hipMemcpyAsync(p->h_results, p->d_results, bytes, hipMemcpyDeviceToHost, st));
     CKH(hipStreamSynchronize(st));
     std::memcpy(out, p->h_results, bytes);
     return TPE_OK;
   }
-  if (!p->h_flag) {
-    CKH(hipHostMalloc((void **)&p->h_flag, 64, hipHostMallocCoherent | hipHostMallocMapped));
-    __atomic_store_n(p->h_flag, (uint64_t)0, __ATOMIC_RELEASE);
-  }
-  const uint64_t seq = ++p->seq;
-  CKH(launch_publish(p->d_results, p->h_results, bytes, p->h_flag, seq, st));
+  // (the call's last launch published already: pub_fired, sequence p->seq)
+  const bool fired = p->pub_fired;
+  p->pub_fired = false;
+  const uint64_t seq = fired ? p->seq : ++p->seq;
+  if (!fired) CKH(launch_publish(p->d_results, p->h_results, bytes, p->h_flag, seq, st));
   // spin on the completion word (a stream synchronize's wake-up is the
   // larger part of a small suggest's host-side wait); every 2^12 polls the
   // stream is asked for an error, so a failed launch cannot spin forever
@@ -1081,6 +1104,25 @@ int copy_results(tpe_engine *h, tpe_plan *p, int64_t n_sug, tpe_result *out, int
     }
   }
   std::memcpy(out, p->h_results, bytes);
+  return TPE_OK;
+}
+
+// the pinned host buffers of a call's results (copy_results; armed before a
+// call whose last launch publishes them itself)
+int host_results(tpe_engine *h, tpe_plan *p, int64_t n_sug) {
+  const size_t bytes = (size_t)n_sug * p->P * sizeof(tpe_result);
+  if (bytes > p->h_results_cap) {
+    if (p->h_results) (void)hipHostFree(p->h_results);
+    p->h_results = nullptr;
+    p->h_results_cap = 0;
+    const size_t cap = std::max<size_t>(bytes, 4096);
+    CKH(hipHostMalloc((void **)&p->h_results, cap, hipHostMallocCoherent | hipHostMallocMapped));
+    p->h_results_cap = cap;
+  }
+  if (publish_on() && !p->h_flag) {
+    CKH(hipHostMalloc((void **)&p->h_flag, 64, hipHostMallocCoherent | hipHostMallocMapped));
+    __atomic_store_n(p->h_flag, (uint64_t)0, __ATOMIC_RELEASE);
+  }
   return TPE_OK;
 }
 
@@ -1722,8 +1764,17 @@ int tpe_plan_fit_suggest(tpe_plan_t p, double gamma, int32_t gamma_cap, double p
     if (n_sug > kInlineSeeds)
       CKH(hipMemcpyAsync(p->d_seeds, seeds, n_sug * 8, hipMemcpyHostToDevice, st));
     if (p->prof_cap > 0) CKH(hipEventRecord(p->ev0, st));
+    // results to the host: the step's last launch may publish them itself
+    // (run_level, tile_draw levels), with the pinned buffers in place first
+    p->pub_fired = false;
+    p->pub_arm = out && !out_on_device && publish_on() && p->prof_cap == 0 && !p->census;
+    if (p->pub_arm) {
+      rc = host_results(h, p, n_sug);
+      if (rc) { p->pub_arm = false; return rc; }
+    }
     rc = enqueue_step(h, p, nb, prior_weight, lf, n_sug, n_cand, st);
-    if (rc) return rc;
+    p->pub_arm = false;
+    if (rc) { p->pub_fired = false; return rc; }
     if (p->prof_cap > 0) CKH(hipEventRecord(p->ev1, st));
     if (graphable && !(p->graph_ok && p->graph_key == key)) {
       p->pending = true;

@@ -280,6 +280,16 @@ struct ScoreArgs {
                              // (k_score_tdraw; no k_draw launch, nothing written)
   const LatInfo *lat_info;   // [P] value lattices (KIND_LAT slots)
   const double2 *lat;        // lattice (lpdf below, lpdf above) pairs
+  // a tile_draw launch that ends its call (pub_flag non-null): the last of its
+  // pub_events final records copies all pub_words words of results into the
+  // pinned pub_dst and then stores pub_seq into *pub_flag -- k_publish's
+  // work without its launch (pub_ticket: a counter, zero between launches)
+  uint64_t *pub_dst;
+  uint64_t *pub_flag;
+  uint32_t *pub_ticket;
+  uint64_t pub_seq;
+  int32_t pub_words;
+  int32_t pub_events;
 };
 
 // Arguments of the fit kernels (tpe_fit.hip), one block per (hp, side) slot.

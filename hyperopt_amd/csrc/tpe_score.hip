@@ -1222,6 +1222,46 @@ __device__ unsigned long long g_rr2_cnt[4];
 __device__ double g_rr2_ex[64][8];
 #endif
 
+// A final record of a tile_draw launch that ends its call (ScoreArgs::pub_*),
+// called by a whole wave after its lane 0 stored the record write-through
+// (store_record_sc1, drained): lane 0 takes an arrival ticket; the wave whose
+// ticket is the launch's last copies every record of the call (agent-scope
+// loads) into the pinned host buffer, then a system-scope release and the
+// sequence word the host spins on -- what k_publish does, one launch less.
+// (The tile records' protocol above: sc1 stores, ticket, sc1 loads, no L2
+// write-back; the diagnostic TPE_REREAD build stores plainly and releases.)
+// Every store is a vector store.
+__device__ __forceinline__ void store_record_sc1(Partial *rr, const Partial &v) {
+  gu64 *w = (gu64 *)(uintptr_t)rr;
+  __hip_atomic_store(w + 0, dbits(v.score), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(w + 1, dbits(v.value), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(w + 2, (uint64_t)v.index, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(w + 3, (uint64_t)(uint32_t)v.active | ((uint64_t)(uint32_t)v.pad << 32),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+__device__ __forceinline__ void publish_arrive(const ScoreArgs &A) {
+  const int lane = threadIdx.x & 63;
+  int last = 0;
+  if (lane == 0) {
+#ifdef TPE_REREAD
+    constexpr int kOrd = __ATOMIC_RELEASE;
+#else
+    constexpr int kOrd = __ATOMIC_RELAXED;
+#endif
+    const uint32_t t = __hip_atomic_fetch_add(A.pub_ticket, 1u, kOrd, __HIP_MEMORY_SCOPE_AGENT);
+    last = t == (uint32_t)A.pub_events - 1 ? 1 : 0;
+    if (last) __hip_atomic_store(A.pub_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (!__shfl(last, 0, 64)) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the loads below the ticket
+  gu64 *src = (gu64 *)(uintptr_t)A.results;
+  for (int i = lane; i < A.pub_words; i += 64)
+    A.pub_dst[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  if (lane == 0) __hip_atomic_store(A.pub_flag, A.pub_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // (SM: ScoreSmem, or ScoreSmem1 for the one-row wave tiles, whose
 // workgroup stages both mixtures' tables in LDS when they fit kStageBlocks)
 template <int KIND, bool CENSUS, typename SM, bool LDRAW = false, bool TDRAW = false>
@@ -1242,6 +1282,16 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
   const bool act = A.force_active || known_active ||
                    hp_active(H, A.results + (int64_t)s * A.n_hp, A.cond_parent, A.cond_branch);
   if (!act) {  // one record says "inactive"; no tickets are taken
+    if constexpr (TDRAW) {  // (its final record: one arrival)
+      if (A.pub_flag) {
+        if (tile == 0 && threadIdx.x < 64) {
+          if (threadIdx.x == 0)
+            store_record_sc1(A.results + (int64_t)s * A.n_hp + hp, Partial{NAN, NAN, -1, 0, 0});
+          publish_arrive(A);
+        }
+        return;
+      }
+    }
     if (tile == 0 && threadIdx.x == 0)
       A.results[(int64_t)s * A.n_hp + hp] = Partial{NAN, NAN, -1, 0, 0};
     return;
@@ -1893,9 +1943,13 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
   wave_best(fs, fv, fi);
   if (lane == 0) {
     Partial *rr = A.results + (int64_t)s * A.n_hp + hp;
-    if (!(A.accumulate && better(rr->score, rr->index, fs, fi))) *rr = Partial{fs, fv, fi, 1, 0};
+    if (TDRAW && A.pub_flag) store_record_sc1(rr, Partial{fs, fv, fi, 1, 0});  // (never accumulating)
+    else if (!(A.accumulate && better(rr->score, rr->index, fs, fi))) *rr = Partial{fs, fv, fi, 1, 0};
   }
 #endif
+  if constexpr (TDRAW) {  // (this slot's final record: one arrival)
+    if (A.pub_flag) publish_arrive(A);
+  }
 }
 
 #ifdef TPE_REREAD

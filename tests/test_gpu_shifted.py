@@ -545,20 +545,21 @@ print('hex', res.view(np.uint8).tobytes().hex())
 
 @pytest.mark.parametrize('env', [{'TPE_LOOKUP_DRAW': '0'}, {'TPE_LOOKUP_FORK': '0'},
                                  {'TPE_SIDE_STREAMS': '1'}, {'TPE_PUBLISH': '0'},
-                                 {'TPE_TILE_DRAW': '0'}],
+                                 {'TPE_TILE_DRAW': '0'}, {'TPE_PUBLISH_FUSE': '0'}],
                          ids=['lookup_from_draw', 'lookup_in_order', 'side_streams', 'no_publish',
-                              'no_tile_draw'])
+                              'no_tile_draw', 'publish_launch'])
 def test_launch_switches_identical_results(env):
     """The launch-shape switches change no result: lookup slots written by
     the sorted draw instead of drawn in their tiles (TPE_LOOKUP_DRAW=0), the
     lookup launch in order instead of forked (TPE_LOOKUP_FORK=0), the forked
     lattice / mixed-level launches (TPE_SIDE_STREAMS=1), the runtime copy
-    of the results (TPE_PUBLISH=0) and k_draw for tiny draws instead of the
-    tiles drawing (TPE_TILE_DRAW=0) -- a config-3 suggest of 1e5 candidates
-    (two levels, lattice and categorical lookups beside log-sum-exp slots),
-    a batched config-2 suggest of 3e5 and tpe.suggest batches of 24 and 1000
-    candidates over a space without quantized hps, identical to the
-    defaults."""
+    of the results (TPE_PUBLISH=0), k_draw for tiny draws instead of the
+    tiles drawing (TPE_TILE_DRAW=0) and k_publish after such a call's last
+    launch instead of that launch publishing (TPE_PUBLISH_FUSE=0) -- a
+    config-3 suggest of 1e5 candidates (two levels, lattice and categorical
+    lookups beside log-sum-exp slots), a batched config-2 suggest of 3e5 and
+    tpe.suggest batches of 24 and 1000 candidates over a space without
+    quantized hps and over a conditional one, identical to the defaults."""
     code = """
 import sys, numpy as np
 sys.path.insert(0, 'tests')
@@ -578,17 +579,22 @@ from hyperopt_amd import hp, tpe, rand, Trials
 from hyperopt_amd.base import Domain
 space = {'u': hp.uniform('u', -3, 2), 'l': hp.loguniform('l', -4, 1),
          'c': hp.choice('c', [0, 1, 2, 3]), 'n': hp.normal('n', 0, 2)}
-dom = Domain(lambda x: 0.0, space)
-t = Trials()
-docs = rand.suggest(list(range(150)), dom, t, 1)
-for d, l in zip(docs, np.random.RandomState(4).rand(150)):
-    d['state'] = 2
-    d['result'] = {'status': 'ok', 'loss': float(l)}
-t._insert_trial_docs(docs)
-t.refresh()
-for n_ei in (24, 1000):
-    got = tpe.suggest(t.new_trial_ids(2), dom, t, 77, n_EI_candidates=n_ei)
-    out.append(repr([sorted(g['misc']['vals'].items()) for g in got]))
+cond = {'k': hp.choice('k', [{'a': hp.uniform('a', 0, 1)},
+                             {'b': hp.normal('b', 0, 1), 'c2': hp.choice('c2', [0, 1])}]),
+        'u': hp.uniform('u', -1, 1)}
+for sp in (space, cond):
+    dom = Domain(lambda x: 0.0, sp)
+    t = Trials()
+    docs = rand.suggest(list(range(150)), dom, t, 1)
+    for d, l in zip(docs, np.random.RandomState(4).rand(150)):
+        d['state'] = 2
+        d['result'] = {'status': 'ok', 'loss': float(l)}
+    t._insert_trial_docs(docs)
+    t.refresh()
+    for n_ei in (24, 1000):
+        for k in (1, 2, 3):
+            got = tpe.suggest(t.new_trial_ids(k), dom, t, 77 + k, n_EI_candidates=n_ei)
+            out.append(repr([sorted(g['misc']['vals'].items()) for g in got]))
 print('hex', ':'.join(out))
 """
     a = _child(code, env)

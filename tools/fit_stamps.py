@@ -24,7 +24,20 @@ def main(cfg, slots):
     import torch
     torch.cuda.set_device(0)
     eng = E.Engine(0)
-    dom, losses, vals, active = bench.build_workload(cfg)
+    if cfg == 'cfg1':  # one uniform hp, 50 finished trials (the config-1 fmin's mid point)
+        from hyperopt_amd import hp, rand, Trials
+        from hyperopt_amd.base import Domain
+        from hyperopt_amd.tpe import build_history
+        dom, t = Domain(lambda x: 0.0, hp.uniform('x', -5, 5)), Trials()
+        docs = rand.suggest(list(range(50)), dom, t, 1)
+        for d, l in zip(docs, np.random.RandomState(2).rand(50)):
+            d['state'] = 2
+            d['result'] = {'status': 'ok', 'loss': float(l)}
+        t._insert_trial_docs(docs)
+        t.refresh()
+        _, losses, vals, active = build_history(dom, t, dom.space.labels)
+    else:
+        dom, losses, vals, active = bench.build_workload(cfg)
     hps, conds, pprior = dom.space.engine_tables()
     plan = E.Plan(eng, hps, conds, pprior, max_trials=losses.size)
     plan.set_history(losses, vals, active)
