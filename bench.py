@@ -445,7 +445,7 @@ def main():
     plan.census(True)
     for i in range(n_prof):
         step(args.warmup + args.steps + n_prof + i)
-    census = plan.census(False, n=10)
+    census = plan.census(False, n=11)
 
     e2e = None
     if rank == 0 and world == 1 and not args.no_e2e:
@@ -484,6 +484,7 @@ def report(args, C, eng, world, mode, elapsed, value, pairs_step, pairs_suggest,
     lse_peak_shift = eng.microbench(6 if args.prune == 3 else 5)
     lse_peak_exact32 = eng.microbench(7)   # mode 3's fp32 per-group-lift pair
     lse_peak_mom = eng.microbench(8)       # mode 3's moment form of a 16-component chunk
+    lse_peak_mom8 = eng.microbench(9)      # ... of an 8-component block (degree 15)
     lse_peak = max(lse_peak_exact, lse_peak_shift, lse_peak_mom if args.prune == 3 else 0.0)
     erf_peak = eng.microbench(4)
     lse_pairs = kinds.get('lse_gmm', 0.0) + kinds.get('lse_lgmm', 0.0)
@@ -492,15 +493,34 @@ def report(args, C, eng, world, mode, elapsed, value, pairs_step, pairs_suggest,
     lse_shift = census[4] / per_launch if census[3] else 0.0   # of which one-exponent form
     lse_exact32 = census[6] / per_launch if census[3] else 0.0  # fp32 per-group-lift form
     lse_mom = census[9] / per_launch if census[3] else 0.0      # of lse_shift: moment form
+    lse_mom8 = census[10] / per_launch if census[3] else 0.0    # of lse_mom: the 8-wide form
     erf_exec = census[2] / per_launch
     t_kernel = score_ms * 1e-3
     # each evaluated pair priced at the register-only rate of the arithmetic
     # it ran: per-group-max lift, one wave exponent, or quantized erf
     t_peak = ((lse_exec - lse_shift - lse_exact32) / lse_peak_exact +
-              (lse_shift - lse_mom) / lse_peak_shift + lse_mom / lse_peak_mom +
+              (lse_shift - lse_mom) / lse_peak_shift + (lse_mom - lse_mom8) / lse_peak_mom +
+              lse_mom8 / lse_peak_mom8 +
               lse_exact32 / lse_peak_exact32 + erf_exec / erf_peak)
     frac = t_peak / t_kernel if t_kernel else None
     achieved = (frac or 0.0) * lse_peak
+    # the same launch in literal SURVEY 8(d) units: v_exp_f32 issued (one per
+    # evaluated pair, one per moment chunk / block and candidate) against the
+    # measured v_exp_f32 peak over the launch time, and VALU instructions
+    # (x 64 lanes) per evaluated pair from the committed SQ pass of this config
+    exp_peak = eng.microbench(0)
+    exp_issued = (lse_exec - lse_mom) + (lse_mom - lse_mom8) / 16.0 + lse_mom8 / 8.0
+    exp_issue_frac = exp_issued / (exp_peak * t_kernel) if t_kernel else None
+    valu_pp, sq_src = None, None
+    if os.path.exists(args.traffic_json):
+        try:
+            with open(args.traffic_json) as f:
+                sq = json.load(f).get(args.config, {})
+            if sq.get('valu_insts_per_launch') and (lse_exec + erf_exec):
+                valu_pp = 64.0 * sq['valu_insts_per_launch'] / (lse_exec + erf_exec)
+                sq_src = sq.get('_sq_source')
+        except Exception:
+            valu_pp = None
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
@@ -525,10 +545,19 @@ def report(args, C, eng, world, mode, elapsed, value, pairs_step, pairs_suggest,
                      'pair below the one-exponent size: the same in fp32 with the group max and '
                      'lift; mode 3 moment form of a 16-component equal-sigma chunk: one exp2 + '
                      'a degree-9 packed fp32 polynomial per candidate and chunk, 16 pairs; '
+                     '8-wide moment form of a block of 8: the same with a degree-15 polynomial, '
+                     '8 pairs; exp_issue_frac = v_exp_f32 issued / (exp_f32 peak x launch time); '
                      'quantized pair: 2 OCML fp64 erf + 8 flops)',
                 lse_evaluated_shifted_pairs_per_launch=lse_shift,
                 lse_evaluated_moment_pairs_per_launch=lse_mom,
+                lse_evaluated_moment8_pairs_per_launch=lse_mom8,
                 lse_pair_moment_peak_per_s=lse_peak_mom,
+                lse_pair_moment8_peak_per_s=lse_peak_mom8,
+                exp_issue_frac=exp_issue_frac, exp_issued_per_launch=exp_issued,
+                valu_per_evaluated_pair=valu_pp,
+                valu_per_evaluated_pair_note=('SQ_INSTS_VALU per scoring launch (x 64 lanes) from '
+                                              '%s / this run\'s evaluated pairs per launch' % sq_src
+                                              if valu_pp else None),
                 lse_shifted_retry_pairs_per_launch=census[7] / per_launch,
                 lse_shifted_wide_block_pairs_per_launch=census[8] / per_launch,
                 lse_evaluated_exact_f32_pairs_per_launch=lse_exact32,

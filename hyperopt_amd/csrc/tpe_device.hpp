@@ -335,6 +335,66 @@ __device__ __forceinline__ void store_lse_moments(CoefM *tm, int64_t k, EnvTerm 
   for (int j = 0; j <= kMomDeg; ++j) b->m[j] = m[j];
 }
 
+// reductions over the 8 lanes of a coefficient block (lane & 7; all 8 active)
+__device__ __forceinline__ double row8_min(double v) {
+  v = fmin(v, dppd<kDppXor1>(v));
+  v = fmin(v, dppd<kDppXor2>(v));
+  return fmin(v, dppd<kDppHalfMirror>(v));
+}
+__device__ __forceinline__ double row8_max(double v) {
+  v = fmax(v, dppd<kDppXor1>(v));
+  v = fmax(v, dppd<kDppXor2>(v));
+  return fmax(v, dppd<kDppHalfMirror>(v));
+}
+__device__ __forceinline__ double row8_sum(double v) {
+  v += dppd<kDppXor1>(v);
+  v += dppd<kDppXor2>(v);
+  return v + dppd<kDppHalfMirror>(v);
+}
+
+// The 8-wide moment form (CoefM8, tpe_internal.hpp) of the coefficient block
+// held by this lane's 8-lane group: the same quantities as store_lse_moments
+// over the block's 8 components (centre = the block's mu' midpoint, as
+// store_lse_envelope's Coef32 centre), degree kMom8Deg.
+__device__ __forceinline__ void store_lse_moments8(CoefM8 *tm, int64_t k, EnvTerm e, bool valid) {
+  const double LN2 = 0.6931471805599453;
+  const double lo = row8_min(valid ? e.m : INFINITY), hi = row8_max(valid ? e.m : -INFINITY);
+  const double amin = row8_min(valid ? e.a2 : INFINITY), amax = row8_max(valid ? e.a2 : -INFINITY);
+  const double cen = lo <= hi ? 0.5 * (lo + hi) : 0.0;
+  const double d = valid ? e.m - cen : 0.0;
+  const double T = valid ? e.c - e.a2 * (d * d) : -INFINITY;
+  const double Tm = row8_max(T == T ? T : INFINITY);
+  const double hh = row8_max(valid ? fabs(d) : 0.0);
+  const bool ok = lo <= hi && amin == amax && amin > 0.0 && amin < 1.0e300 && Tm > -1.0e300 &&
+                  Tm < 1.0e300 && hh < 1.0e300;
+  const double rho = (valid && ok) ? exp2(T - Tm) : 0.0;
+  const double q = 2.0 * amin * LN2 * d;
+  float m[kMom8Deg + 1];
+  double p = rho, fact = 1.0;
+#pragma unroll
+  for (int j = 0; j <= kMom8Deg; ++j) {
+    if (j > 0) fact *= (double)j;
+    m[j] = (float)(row8_sum(p) / fact);
+    p *= q;
+  }
+  if (k % kCoefBlock) return;
+  CoefM8 *b = tm + k / kCoefBlock;
+  const double base = ok ? floor(Tm) : 0.0;
+  float xh = INFINITY;
+  if (ok) {
+    const double x = hh * 2.0 * amin * LN2;
+    xh = (float)x;
+    if ((double)xh < x) xh = nextafterf(xh, INFINITY);
+  }
+  b->center = cen;
+  b->xh = xh;
+  b->base = (float)base;
+  b->cm = (float)(Tm - base);
+  b->gam = (float)(-amin);
+#pragma unroll
+  for (int j = 0; j <= kMom8Deg; ++j) b->m[j] = m[j];
+}
+
 // Natural log of a finite x > 0 in ~30 VALU (OCML's fp64 log is ~70: its
 // double-double tail buys the last half-ulp, which no caller here needs --
 // candidate transforms y = log x, the EI ratio, bucketing keys): x = m 2^e

@@ -273,6 +273,62 @@ __device__ double draw_table(const tpe_hp &H, int K, const double *__restrict__ 
   return draw_table_from(H, K, mu, sg, T, draw_block0(seed, gi, stream), seed, gi, stream);
 }
 
+// pick_cdf's index without its loop, for tables of <= CAP components: the
+// number of k < K - 1 with cdf[k] <= t (the CDF is nondecreasing, so that
+// count is the first k with cdf[k] > t, capped at K - 1 -- pick_cdf's value),
+// by a fixed ladder of halving steps (one LDS read and a select each)
+template <int CAP>
+__device__ __forceinline__ int pick_cdf_ladder(const double *cdf, int K, double t) {
+  static_assert((CAP & (CAP - 1)) == 0, "power-of-two table");
+  int lo = 0;
+#pragma unroll
+  for (int step = CAP / 2; step > 0; step >>= 1) {
+    const int j = lo + step;
+    // (the read is in the table whatever K is: no branch around it)
+    const bool ok = (j <= K - 1) & (cdf[min(j, CAP) - 1] <= t);
+    lo = ok ? j : lo;
+  }
+  return lo;
+}
+
+// The bounded continuous draw of draw_table_from (GMM / LGMM, truncated to
+// [low, high)) for the sorted-draw loop, inline: the descriptor fields are
+// wave-uniform arguments (scalar registers, no per-draw descriptor loads or
+// call), the pick is the loop-free ladder, the tail branch a select.  The
+// arithmetic is draw_table_from's, operation for operation, so the values
+// are the same bits (the regeneration tests compare every winner with
+// tpe_sample's draw_table).  cdf_last = T.cdf[K - 1]; high_prev =
+// nextafter(high, -inf).
+template <int CAP>
+__device__ __forceinline__ double draw_bounded_inline(const DrawTableT<CAP> &T, int K,
+                                                      double cdf_last,
+                                                      const double *__restrict__ mu,
+                                                      const double *__restrict__ sg, double low,
+                                                      double high, double high_prev, bool logn,
+                                                      bool hasq, double qv, U4 r0) {
+  const double u0 = u53(r0.x, r0.y), u1 = u53(r0.z, r0.w);
+  const int k = pick_cdf_ladder<CAP>(T.cdf, K, u0 * cdf_last);
+  const double s2 = 1.4142135623730951 * sg[k], b = T.base[k], m = T.mass[k];
+  const int md = T.mode[k];
+  // (draw_table_from's codegen: u1 m once, b -/+ it unfused; x by one fma)
+  double pu, pp;
+  {
+#pragma clang fp contract(off)
+    const double um = u1 * m;
+    pu = b - um;
+    pp = b + um;
+  }
+  const bool lower = md != 1 && (md == 2 || pp < 0.5);
+  const double q = md == 1 ? pu : lower ? pp : 1.0 - pp;
+  const double side = lower ? -1.0 : 1.0;
+  double x = fma(side * s2, erfcinv_fast(2.0 * q), mu[k]);
+  if (!(x >= low)) x = low;
+  if (!(x < high)) x = high_prev;
+  if (logn) x = exp(x);
+  if (hasq) x = rint(x / qv) * qv;
+  return x;
+}
+
 // s is wave-uniform: select the inline seed with an unrolled compare chain
 // (a dynamic index into the by-value argument would copy it to scratch)
 __device__ __forceinline__ uint64_t suggestion_seed(const ScoreArgs &A, int s) {
@@ -411,15 +467,19 @@ constexpr int kSortBuckets = 256;
 // order; per (wave, bucket) counts from 8-ballot lane matching, one scan
 // over (bucket, wave), then the same walk writes the destinations.
 // cnt: NW * 256 ints of LDS; every thread of the block calls it.
+// (per bit: the lane's bit sign-extended, its ballot, and the lanes that
+// differ in it -- ballot xor the lane's own bit -- or-ed into a mismatch
+// mask; three 32-bit ops per half instead of a 64-bit select per bit)
 __device__ __forceinline__ uint64_t lanes_equal8(uint32_t d, bool v) {
-  uint64_t m = __ballot(v);
+  uint32_t mlo = 0u, mhi = 0u;
 #pragma unroll
   for (int b = 0; b < 8; ++b) {
-    const bool x = (d >> b) & 1u;
-    const uint64_t bb = __ballot(x);
-    m &= x ? bb : ~bb;
+    const uint32_t x = (uint32_t)__builtin_amdgcn_sbfe((int)d, b, 1);  // 0 or ~0
+    const uint64_t bb = __ballot(x != 0u);
+    mlo |= (uint32_t)bb ^ x;
+    mhi |= (uint32_t)(bb >> 32) ^ x;
   }
-  return m;
+  return __ballot(v) & ~(((uint64_t)mhi << 32) | mlo);
 }
 
 template <int NW, typename Dest>
@@ -520,25 +580,49 @@ __device__ __forceinline__ void sorted_block_body(const ScoreArgs &A, int slot, 
   double *out = const_cast<double *>(A.cand) + off;
   const int t = threadIdx.x;
   double lo = INFINITY, hi = -INFINITY;
-#pragma unroll 1
-  for (int i = t; i < n; i += NT) {
-    const uint64_t gi = (uint64_t)(A.cand_begin + base + i);
-    double x;
-    if constexpr (EXT) {
-      (void)gi; (void)seed; (void)bw;
-      x = src[(int64_t)slot * A.n_cand + base + i];
-    } else {
-      x = tab ? draw_table_ool<CAP>(A.hps + hp, K, bmu, bsg, &L.T,
-                                    draw_block0(seed, gi, (uint32_t)hp), seed, gi, (uint32_t)hp)
-              : draw_one_ool(A.hps + hp, A.info + sb, bw, bmu, bsg, seed, gi, (uint32_t)hp);
-    }
+  // each candidate: to the output (unbucketed slot) or to the LDS staging
+  // with its bucketing key folded into the block range
+  auto emit = [&](int i, double x) {
     if (!bucket) {
       out[i] = x;
-      continue;
+      return;
     }
     L.xs[i] = x;
     const double key = lg ? fast_log(x) : x;
     if (fabs(key) < INFINITY) { lo = fmin(lo, key); hi = fmax(hi, key); }
+  };
+  // bounded continuous slots with a table (config 4 / 5's hps): the table
+  // draw inline with the descriptor in scalar registers (draw_bounded_inline,
+  // the same values); everything else through the out-of-line draws
+  const bool fast = !EXT && tab && H.family != TPE_CAT && (H.flags & TPE_HAS_LOW) &&
+                    (H.flags & TPE_HAS_HIGH);
+  if (fast) {
+    const double cdf_last = L.T.cdf[K - 1];
+    const double high_prev = nextafter(H.high, -INFINITY);
+    const bool logn = H.family == TPE_LGMM, hasq = (H.flags & TPE_HAS_Q) != 0;
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll 1
+    for (int i = t; i < n; i += NT) {
+      const uint64_t gi = (uint64_t)(A.cand_begin + base + i);
+      const U4 r0 = philox(U4{(uint32_t)gi, (uint32_t)(gi >> 32), (uint32_t)hp, 0u}, k0, k1);
+      emit(i, draw_bounded_inline<CAP>(L.T, K, cdf_last, bmu, bsg, H.low, H.high, high_prev,
+                                       logn, hasq, H.q, r0));
+    }
+  } else {
+#pragma unroll 1
+    for (int i = t; i < n; i += NT) {
+      const uint64_t gi = (uint64_t)(A.cand_begin + base + i);
+      double x;
+      if constexpr (EXT) {
+        (void)gi; (void)seed; (void)bw;
+        x = src[(int64_t)slot * A.n_cand + base + i];
+      } else {
+        x = tab ? draw_table_ool<CAP>(A.hps + hp, K, bmu, bsg, &L.T,
+                                      draw_block0(seed, gi, (uint32_t)hp), seed, gi, (uint32_t)hp)
+                : draw_one_ool(A.hps + hp, A.info + sb, bw, bmu, bsg, seed, gi, (uint32_t)hp);
+      }
+      emit(i, x);
+    }
   }
   if (!bucket) return;
   // block range of the finite keys

@@ -119,6 +119,8 @@ struct tpe_plan {
   Coef *d_coef = nullptr;
   Coef32 *d_coef32 = nullptr;  // [2P][kcap / kCoefBlock] block-local fp32 LSE terms
   CoefM *d_coefm = nullptr;    // [2P][mom_stride(kcap)] moment form of 16-component chunks
+  CoefM8 *d_coefm8 = nullptr;  // [2P][kcap / kCoefBlock] moment form of 8-component blocks
+  std::vector<double> act_frac;  // per hp: expected share of the trials it is active in
   int64_t n = 0;  // history length
   // suggestion state
   int64_t s_cap = 0;
@@ -187,7 +189,8 @@ struct tpe_plan {
   StepKey graph_key, pending_key;
   bool graph_ok = false, pending = false;
   bool capturing = false;  // enqueue_step under graph capture (no per-call patch of score seeds)
-  bool mom_fresh = false;  // the last fit wrote the moment table (fit_args)
+  int32_t mom_w = 0;       // moment table the last fit wrote: 16 (CoefM), 8 (CoefM8), 0 none
+  int32_t graph_mom_w = 0; // ... the captured graph's fit (launch_step restores it)
   HistPatch pend{};        // a small history update not yet on the device: the next
   bool has_pend = false;   // fit writes it (k_fit's patch), anything else flushes it
   hipGraph_t graph = nullptr;
@@ -246,7 +249,8 @@ void plan_free_buffers(tpe_plan *p) {
                   p->d_losses, p->d_vals, p->d_active, p->d_below, p->d_mw, p->d_mmu,
                   p->d_msig, p->d_scratch, p->d_info, p->d_coef, p->d_results, p->d_seeds,
                   p->d_partial, p->d_ext, p->d_lb, p->d_la, p->d_cand, p->d_cpos,
-                  p->d_ticket, p->d_sortbuf, p->d_census, p->d_lat_info, p->d_lat, p->d_coef32, p->d_coefm};
+                  p->d_ticket, p->d_sortbuf, p->d_census, p->d_lat_info, p->d_lat, p->d_coef32, p->d_coefm,
+                  p->d_coefm8};
   for (void *b : bufs) dfree(b);
   if (p->h_results) (void)hipHostFree(p->h_results);
   p->h_results = nullptr;
@@ -427,6 +431,23 @@ int plan_build(tpe_engine *h, const tpe_space *sp, int64_t max_trials, tpe_plan 
   CKH(dalloc(&p->d_coef, (size_t)slots * kcap));
   CKH(dalloc(&p->d_coef32, (size_t)slots * (kcap / kCoefBlock)));
   CKH(dalloc(&p->d_coefm, (size_t)slots * mom_stride(kcap)));
+  CKH(dalloc(&p->d_coefm8, (size_t)slots * (kcap / kCoefBlock)));
+  // expected activity of every hp (mom_width): an hp conditioned on branch b
+  // of a categorical parent is active in ~1 / upper of the parent's trials
+  // (levels are in dependency order: parents first)
+  p->act_frac.assign(p->P, 1.0);
+  for (const auto &lv : p->levels)
+    for (int i : lv) {
+      const tpe_hp &x = p->hps[i];
+      if (x.cond_count == 0) continue;
+      double f = 0.0;
+      for (int c = 0; c < x.cond_count; ++c) {
+        const int par = p->cond_parent[x.cond_begin + c];
+        const tpe_hp &y = p->hps[par];
+        f += p->act_frac[par] / (y.family == TPE_CAT ? std::max(1, (int)y.upper) : 1);
+      }
+      p->act_frac[i] = std::min(1.0, f);
+    }
   CKH(hipEventCreate(&p->ev0));
   CKH(hipEventCreate(&p->ev1));
   CKH(hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming));
@@ -616,6 +637,7 @@ ScoreArgs base_args(tpe_plan *p, int64_t n_sug) {
   a.coef = p->d_coef;
   a.coef32 = p->d_coef32;
   a.coefm = p->d_coefm;
+  a.coefm8 = p->d_coefm8;
   a.mw = p->d_mw;
   a.mmu = p->d_mmu;
   a.msig = p->d_msig;
@@ -629,14 +651,35 @@ ScoreArgs base_args(tpe_plan *p, int64_t n_sug) {
   a.n_suggest = (int32_t)n_sug;
   a.lat_info = p->d_lat_info;
   a.lat = p->d_lat;
-  a.lse_mom = moment_on() && p->mom_fresh ? 1 : 0;
+  a.lse_mom = p->mom_w;
   return a;
 }
 
-// mom: write the moment table (CoefM) -- only the wave tiles of sorted draws
-// read it; plan.mom_fresh records whether the tables hold it
+// The moment width of the plan's log-sum-exp mixtures (tpe_internal.hpp
+// CoefM8): 16 when the largest expected above-side mixture (history length
+// x the hp's expected activity) has >= kMom16MinK components (neighbour gaps
+// << sigma floor: 16-component chunks qualify), 8 from the one-exponent size
+// (lse_shift_min) up, else 0.  (tools/moment_error.py: at N = 5000 the 16-wide
+// form covers 72 % of the live chunks at 0.6 VALU per pair, the 8-wide 99 %
+// at ~1.7; at N = 3000, 36 % against 98 %.)  A function of the plan and its
+// history length only, so tpe_plan_fit and fit_suggest write the same table.
+int32_t mom_width(const tpe_plan *p) {
+  if (!moment_on()) return 0;
+  double kmax = 0.0;
+  for (int i = 0; i < p->P; ++i) {
+    const int k = score_kind(p->hps[i]);
+    if (k == KIND_LSE_G || k == KIND_LSE_L) kmax = std::max(kmax, (double)p->n * p->act_frac[i]);
+  }
+  if (kmax >= (double)kMom16MinK) return 16;
+  if (kmax >= (double)lse_shift_min()) return 8;
+  return 0;
+}
+
+// mom: write the moment table of the plan's width (mom_width) -- only the
+// wave tiles of sorted draws read it; plan.mom_w records which one the tables
+// hold (the scoring launches read that one: base_args)
 FitArgs fit_args(tpe_plan *p, int32_t n_below, double prior_weight, int32_t lf, bool mom = true) {
-  p->mom_fresh = mom;
+  p->mom_w = mom ? mom_width(p) : 0;
   FitArgs a{};
   a.hps = p->d_hps;
   a.vals = p->d_vals;
@@ -654,7 +697,8 @@ FitArgs fit_args(tpe_plan *p, int32_t n_below, double prior_weight, int32_t lf, 
   a.info = p->d_info;
   a.coef = p->d_coef;
   a.coef32 = p->d_coef32;
-  a.coefm = mom ? p->d_coefm : nullptr;
+  a.coefm = p->mom_w == 16 ? p->d_coefm : nullptr;
+  a.coefm8 = p->mom_w == 8 ? p->d_coefm8 : nullptr;
   a.kcap = p->kcap;
   a.ob = p->d_scratch;
   a.tmp = p->d_scratch;
@@ -1099,8 +1143,16 @@ int copy_results(tpe_engine *h, tpe_plan *p, int64_t n_sug, tpe_result *out, int
     if ((it & 4095) == 0) {
       const hipError_t q = hipStreamQuery(st);
       if (q != hipSuccess && q != hipErrorNotReady) return fail(h, TPE_E_HIP, hipGetErrorString(q));
-      if (q == hipSuccess && __atomic_load_n(p->h_flag, __ATOMIC_ACQUIRE) != seq)
+      if (q == hipSuccess && __atomic_load_n(p->h_flag, __ATOMIC_ACQUIRE) != seq) {
+        // a fused publish short of arrivals leaves its launch-wide ticket
+        // counting: clear it, or the next fused publish of this plan would
+        // fire early and copy records not yet written
+        if (fired) {
+          (void)hipMemsetAsync(p->d_ticket + (size_t)p->s_cap * p->P, 0, sizeof(uint32_t), st);
+          (void)hipStreamSynchronize(st);
+        }
         return fail(h, TPE_E_HIP, "k_publish finished without its completion word");
+      }
     }
   }
   std::memcpy(out, p->h_results, bytes);
@@ -1359,8 +1411,9 @@ int tpe_score(tpe_handle_t h, int32_t family, const double *x, int64_t n, const 
   if (rc) return rc;
   rc = put_mixture(h, p, 1, wa, ma, sa, ka, kind);
   if (rc) return rc;
-  CKH(launch_prep(p->d_hps, 1, p->d_mw, p->d_mmu, p->d_msig, p->d_info, p->d_coef, p->d_coef32, p->d_coefm, p->kcap,
-                  p->d_scratch, h->stream));
+  CKH(launch_prep(p->d_hps, 1, p->d_mw, p->d_mmu, p->d_msig, p->d_info, p->d_coef, p->d_coef32,
+                  p->d_coefm, nullptr, p->kcap, p->d_scratch, h->stream));
+  p->mom_w = moment_on() ? 16 : 0;
   rc = ensure_ext(h, p, n);
   if (rc) return rc;
   CKH(hipMemcpyAsync(p->d_ext, x, n * 8, hipMemcpyHostToDevice, h->stream));
@@ -1407,8 +1460,9 @@ int tpe_sample(tpe_handle_t h, int32_t family, const double *w, const double *mu
   if (rc) return rc;
   rc = put_mixture(h, p, 1, w, mu, sigma, k, kind);
   if (rc) return rc;
-  CKH(launch_prep(p->d_hps, 1, p->d_mw, p->d_mmu, p->d_msig, p->d_info, p->d_coef, p->d_coef32, p->d_coefm, p->kcap,
-                  p->d_scratch, h->stream));
+  CKH(launch_prep(p->d_hps, 1, p->d_mw, p->d_mmu, p->d_msig, p->d_info, p->d_coef, p->d_coef32,
+                  p->d_coefm, nullptr, p->kcap, p->d_scratch, h->stream));
+  p->mom_w = moment_on() ? 16 : 0;
   rc = ensure_ext(h, p, n);
   if (rc) return rc;
   CKH(launch_sample(p->d_hps, p->d_mw, p->d_mmu, p->d_msig, p->d_info, seed, stream, offset, n,
@@ -1525,7 +1579,7 @@ int tpe_plan_fit(tpe_plan_t p, double gamma, int32_t gamma_cap, double prior_wei
   hipStream_t st = pick_stream(h, stream);
   const double nbf = std::ceil(gamma * std::sqrt((double)p->n));
   const int32_t nb = (int32_t)std::max(0.0, std::min<double>(nbf, gamma_cap));
-  const int rc = fit_launch(h, p, fit_args(p, nb, prior_weight, lf, moment_on()), p->P, st);
+  const int rc = fit_launch(h, p, fit_args(p, nb, prior_weight, lf, true), p->P, st);
   if (rc) return rc;
   p->last_nb = nb;
   return TPE_OK;
@@ -1553,7 +1607,7 @@ int tpe_plan_get_table(tpe_plan_t p, int32_t hp, int32_t side, int32_t which, vo
                        int64_t cap_bytes, int64_t *bytes) {
   if (!p || !bytes) return TPE_E_INVALID;
   tpe_engine *h = p->eng;
-  if (hp < 0 || hp >= p->P || side < 0 || side > 1 || which < 0 || which > 2)
+  if (hp < 0 || hp >= p->P || side < 0 || side > 1 || which < 0 || which > 3)
     return fail(h, TPE_E_INVALID, "bad hp/side/table");
   CKH(hipSetDevice(h->device));
   CKH(hipDeviceSynchronize());
@@ -1565,9 +1619,12 @@ int tpe_plan_get_table(tpe_plan_t p, int32_t hp, int32_t side, int32_t which, vo
   } else if (which == 1) {
     *bytes = p->kcap / kCoefBlock * (int64_t)sizeof(Coef32);
     src = p->d_coef32 + slot * (p->kcap / kCoefBlock);
-  } else {
+  } else if (which == 2) {
     *bytes = mom_stride(p->kcap) * (int64_t)sizeof(CoefM);
     src = p->d_coefm + slot * mom_stride(p->kcap);
+  } else {
+    *bytes = p->kcap / kCoefBlock * (int64_t)sizeof(CoefM8);
+    src = p->d_coefm8 + slot * (p->kcap / kCoefBlock);
   }
   if (!out) return TPE_OK;
   if (*bytes > cap_bytes) return fail(h, TPE_E_INVALID, "capacity too small");
@@ -1620,17 +1677,15 @@ namespace {
 int enqueue_step(tpe_engine *h, tpe_plan *p, int32_t nb, double prior_weight, int32_t lf,
                  int64_t n_sug, int64_t n_cand, hipStream_t st) {
   // the moment table only for a step whose suggest takes a sorted draw
-  // (run_level's sorted_draw: n_cand x n_sug x level hps >= 2^22) on
-  // two-row wave tiles; the others skip its ~3-5 us in k_fit
-  // -- and two-row wave tiles: the one-row tiles of <= kWaveRowSplitMax
-  // candidates find few chunks narrow enough (config 3: 5 % of its pairs)
-  bool mom = n_cand > kWaveRowSplitMax;
+  // (run_level's sorted_draw: n_cand x n_sug x level hps >= 2^22), the only
+  // launches that read it; the others skip its ~3-5 us in k_fit.  Whenever it
+  // is read, the table is the one tpe_plan_fit writes (mom_width), so a
+  // fit_suggest and a fit + suggest score alike (test_fit_suggest_matches_*)
   bool sorted = false;
   for (const auto &l : p->levels)
     sorted |= n_cand * n_sug * (int64_t)l.size() >= ((int64_t)1 << 22);
-  mom = mom && sorted;
   {
-    const int rc = fit_launch(h, p, fit_args(p, nb, prior_weight, lf, mom && moment_on()), p->P, st);
+    const int rc = fit_launch(h, p, fit_args(p, nb, prior_weight, lf, sorted), p->P, st);
     if (rc) return rc;
   }
   p->last_nb = nb;
@@ -1656,6 +1711,7 @@ int capture_step(tpe_engine *h, tpe_plan *p, int32_t nb, double prior_weight, in
     return rc ? rc : fail(h, TPE_E_HIP, "graph capture failed");
   }
   p->graph = g;
+  p->graph_mom_w = p->mom_w;  // the table the captured fit writes (its args are fixed)
   CKH(hipGraphInstantiate(&p->graph_exec, g, nullptr, nullptr, 0));
   size_t nn = 0;
   CKH(hipGraphGetNodes(g, nullptr, &nn));
@@ -1723,6 +1779,7 @@ int launch_step(tpe_engine *h, tpe_plan *p, int32_t nb, const uint64_t *seeds, i
   }
   CKH(hipGraphLaunch(p->graph_exec, st));
   p->last_nb = nb;
+  p->mom_w = p->graph_mom_w;  // (no fit_args on replay: the captured fit's table)
   return TPE_OK;
 }
 
@@ -1774,7 +1831,14 @@ int tpe_plan_fit_suggest(tpe_plan_t p, double gamma, int32_t gamma_cap, double p
     }
     rc = enqueue_step(h, p, nb, prior_weight, lf, n_sug, n_cand, st);
     p->pub_arm = false;
-    if (rc) { p->pub_fired = false; return rc; }
+    if (rc) {
+      // (a publishing launch that went out counts its arrivals: clear the
+      // ticket for the plan's next fused publish)
+      if (p->pub_fired)
+        (void)hipMemsetAsync(p->d_ticket + (size_t)p->s_cap * p->P, 0, sizeof(uint32_t), st);
+      p->pub_fired = false;
+      return rc;
+    }
     if (p->prof_cap > 0) CKH(hipEventRecord(p->ev1, st));
     if (graphable && !(p->graph_ok && p->graph_key == key)) {
       p->pending = true;
@@ -2055,7 +2119,7 @@ int tpe_plan_set_prune(tpe_plan_t p, int32_t mode) {
 }
 
 int tpe_microbench(tpe_handle_t h, int32_t which, double *per_second) {
-  if (!h || !per_second || which < 0 || which > 8) return TPE_E_INVALID;
+  if (!h || !per_second || which < 0 || which > 9) return TPE_E_INVALID;
   CKH(hipSetDevice(h->device));
   hipDeviceProp_t prop;
   CKH(hipGetDeviceProperties(&prop, h->device));
@@ -2080,8 +2144,8 @@ int tpe_microbench(tpe_handle_t h, int32_t which, double *per_second) {
   // (4 candidates x 8 components), quantized pairs (2 chains), shifted LSE
   // pairs (4 x 8), block-local fp32 one-exponent LSE pairs (4 x 2 blocks of
   // 8), the fp32 per-group-lift pairs (4 x 8), moment-form pairs (4 x 2
-  // chunks of 16)
-  static const double per_iter[9] = {8.0, 16.0, 4.0, 32.0, 2.0, 32.0, 64.0, 32.0, 128.0};
+  // chunks of 16), 8-wide moment-form pairs (4 x 2 blocks of 8)
+  static const double per_iter[10] = {8.0, 16.0, 4.0, 32.0, 2.0, 32.0, 64.0, 32.0, 128.0, 64.0};
   *per_second = 4.0 * blocks * 256.0 * iters * per_iter[which] / (ms * 1e-3);
   return TPE_OK;
 }

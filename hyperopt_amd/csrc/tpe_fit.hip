@@ -809,7 +809,7 @@ __device__ __forceinline__ Split compute_split(const FitArgs &A, const FitCtx &C
 // padding components of the last block (alpha = -inf: terms exactly 0).
 // ------------------------------------------------------------------------
 __device__ __forceinline__ void store_table(const tpe_hp &H, Coef *cf, Coef32 *cf32, CoefM *cfm,
-                                            int K, const double *w, const double *mu,
+                                            CoefM8 *cfm8, int K, const double *w, const double *mu,
                                             const double *sg, double pacc, bool quant) {
   const int kp = (K + kCoefBlock - 1) / kCoefBlock * kCoefBlock;
   const int kp16 = (K + kMomChunk - 1) / kMomChunk * kMomChunk;
@@ -826,6 +826,7 @@ __device__ __forceinline__ void store_table(const tpe_hp &H, Coef *cf, Coef32 *c
     if (k < kp) {
       store_coef(cf, k, c, quant);
       if (!quant) store_lse_envelope(cf, k, e, real, c, cf32);
+      if (!quant && cfm8) store_lse_moments8(cfm8, k, e, real);
     }
     if (!quant && cfm) store_lse_moments(cfm, k, e, real);
   }
@@ -839,11 +840,13 @@ __device__ __forceinline__ void store_table(const tpe_hp &H, Coef *cf, Coef32 *c
 // would put that copy on the scratch stack when the call is not inlined)
 __device__ __forceinline__ void prep_slot(const tpe_hp *Hg, int64_t slot, int K, const double *w, const double *mu,
                           const double *sg, MixInfo *info, Coef *coef, Coef32 *coef32,
-                          CoefM *coefm, int64_t kcap, double *tmp, FitShared &sm) {
+                          CoefM *coefm, CoefM8 *coefm8, int64_t kcap, double *tmp,
+                          FitShared &sm) {
   const tpe_hp H = *Hg;
   Coef *cf = coef + slot * kcap;
   Coef32 *cf32 = coef32 + slot * (kcap / kCoefBlock);
-  CoefM *cfm = coefm + slot * mom_stride(kcap);
+  CoefM *cfm = coefm ? coefm + slot * mom_stride(kcap) : nullptr;
+  CoefM8 *cfm8 = coefm8 ? coefm8 + slot * (kcap / kCoefBlock) : nullptr;
   const double wsum = block_np_sum(w, K, sm);
   STAMP(7);
   if (H.family == TPE_CAT) {
@@ -870,7 +873,7 @@ __device__ __forceinline__ void prep_slot(const tpe_hp *Hg, int64_t slot, int K,
   }
   STAMP(8);
   const bool quant = (H.flags & TPE_HAS_Q) != 0;
-  store_table(H, cf, cf32, cfm, K, w, mu, sg, pacc, quant);
+  store_table(H, cf, cf32, cfm, cfm8, K, w, mu, sg, pacc, quant);
   if (threadIdx.x == 0) {
     MixInfo mi;
     mi.K = K; mi.kind = quant ? 1 : 0; mi.p_accept = pacc; mi.log_pacc = log(pacc);
@@ -972,9 +975,10 @@ __device__ __forceinline__ void fit_continuous(const FitArgs &A, const FitCtx &C
   Coef *cf = A.coef + slot * A.kcap;
   Coef32 *cf32 = A.coef32 + slot * (A.kcap / kCoefBlock);
   CoefM *cfm = A.coefm ? A.coefm + slot * mom_stride(A.kcap) : nullptr;
+  CoefM8 *cfm8 = A.coefm8 ? A.coefm8 + slot * (A.kcap / kCoefBlock) : nullptr;
   if (MIXLDS)
     for (int k = threadIdx.x; k < K; k += blockDim.x) { gw[k] = w[k]; gm[k] = mu[k]; gs[k] = sg[k]; }
-  store_table(H, cf, cf32, cfm, K, w, mu, sg, pacc, quant);
+  store_table(H, cf, cf32, cfm, cfm8, K, w, mu, sg, pacc, quant);
   if (threadIdx.x == 0) {
     MixInfo mi;
     mi.K = K; mi.kind = quant ? 1 : 0; mi.p_accept = pacc; mi.log_pacc = log(pacc);
@@ -1129,8 +1133,8 @@ __device__ __forceinline__ void categorical_tail(const FitArgs &A, FitShared &sm
     sg[c] = 0.0;
   }
   __syncthreads();
-  prep_slot(A.hps + slot / 2, slot, upper, w, mu, sg, A.info, A.coef, A.coef32, A.coefm, A.kcap,
-            A.tmp + slot * A.kcap, sm);
+  prep_slot(A.hps + slot / 2, slot, upper, w, mu, sg, A.info, A.coef, A.coef32, A.coefm, A.coefm8,
+            A.kcap, A.tmp + slot * A.kcap, sm);
 }
 
 // ------------------------------------------------------------------------
@@ -1380,7 +1384,8 @@ __global__ __launch_bounds__(256) void k_prep(const tpe_hp *__restrict__ hps,
                                               const double *__restrict__ msig,
                                               MixInfo *__restrict__ info, Coef *__restrict__ coef,
                                               Coef32 *__restrict__ coef32,
-                                              CoefM *__restrict__ coefm, int64_t kcap,
+                                              CoefM *__restrict__ coefm,
+                                              CoefM8 *__restrict__ coefm8, int64_t kcap,
                                               double *__restrict__ scratch) {
   __shared__ FitShared sm;
   const int hp = blockIdx.x, side = blockIdx.y;
@@ -1388,7 +1393,7 @@ __global__ __launch_bounds__(256) void k_prep(const tpe_hp *__restrict__ hps,
   const int K = info[slot].K;
   __syncthreads();
   prep_slot(hps + hp, slot, K, mw + slot * kcap, mmu + slot * kcap, msig + slot * kcap, info, coef,
-            coef32, coefm, kcap, scratch + slot * kcap, sm);
+            coef32, coefm, coefm8, kcap, scratch + slot * kcap, sm);
 }
 
 // ------------------------------------------------------------------------
@@ -1424,10 +1429,11 @@ hipError_t launch_split(const FitArgs &a, uint8_t *below, hipStream_t st) {
 
 hipError_t launch_prep(const tpe_hp *hps, int32_t n_hp, const double *mw, const double *mmu,
                        const double *msig, MixInfo *info, Coef *coef, Coef32 *coef32,
-                       CoefM *coefm, int64_t kcap, double *scratch, hipStream_t st) {
+                       CoefM *coefm, CoefM8 *coefm8, int64_t kcap, double *scratch,
+                       hipStream_t st) {
   if (n_hp <= 0) return hipSuccess;
-  k_prep<<<dim3(n_hp, 2), 256, 0, st>>>(hps, mw, mmu, msig, info, coef, coef32, coefm, kcap,
-                                        scratch);
+  k_prep<<<dim3(n_hp, 2), 256, 0, st>>>(hps, mw, mmu, msig, info, coef, coef32, coefm, coefm8,
+                                        kcap, scratch);
   return hipGetLastError();
 }
 

@@ -107,8 +107,9 @@ constexpr float kLseDeadBase = 26.0f;
 // block-local fp32 per-group-lift form / one-exponent pairs of a wave's
 // second attempt (re-centred exponent) / one-exponent pairs of wide blocks
 // (the fp64 loop of mode 3) / one-exponent pairs evaluated in the moment
-// form of their chunk (CoefM)
-constexpr int kCensus = 10;
+// form of their chunk (CoefM, 16-wide, or CoefM8, 8-wide) / of those, the
+// 8-wide ones
+constexpr int kCensus = 11;
 
 // Per-component scoring coefficients (make_coef, tpe_device.hpp), 4 fields:
 //   LSE: x = alpha, y = beta, z = gamma (t = alpha + y'(beta + gamma y'))
@@ -194,6 +195,33 @@ __host__ __device__ constexpr int64_t mom_stride(int64_t kcap) {
   return (kcap + kMomChunk - 1) / kMomChunk;
 }
 
+// The same moment form per coefficient block of 8 components with a
+// degree-15 polynomial (CoefM8): for mixtures of ~1e3 components (configs 2,
+// 3 and 5: neighbour gaps ~1e-2 against a sigma floor of 0.1) a 16-component
+// chunk spans too much of sigma for the degree-9 bound (xh ~ 7.5, almost no
+// chunk qualifies), while 8 components at degree 15 cover ~60-90 % of the
+// live blocks (tools/moment_error.py MOM_CH=8 MOM_P=15: 1.0e-7 max relative
+// lpdf error against the oracle).  The per-plan width (tpe_engine.hip
+// mom_width): 16 for mixtures of >= kMom16MinK components, else 8 from the
+// one-exponent size up; the scoring kernels are instantiated per width, so the
+// 16-wide kernel's register allocation is the round-5 one.  A block of 8 is
+// one Coef32 block: the same centre (mu' midpoint) and base.  Truncation
+// tau(x) = x^16 / 16! e^x; taken for x <= kMomXLim (tau <= 1e-16) or by the
+// weighted criterion as the 16-wide form.  128 B = two 64-B scalar loads.
+constexpr int kMom8Deg = 15;
+constexpr float kMom8Log2Fact = 44.25014f;  // log2(16!)
+constexpr int64_t kMom16MinK = 4000;
+struct __attribute__((aligned(128))) CoefM8 {
+  double center;   // mu' midpoint of the block (fp64), as Coef32::center
+  float xh;        // max_k |q_k| (nats per unit v), rounded up; +inf: not eligible
+  float base;      // integer near T*
+  float cm;        // T* - base
+  float gam;       // -a^2 (log2 units)
+  float m[kMom8Deg + 1];
+  float pad[8];
+};
+static_assert(sizeof(CoefM8) == 128, "two 64-B scalar loads");
+
 struct Partial {  // == tpe_result layout
   double score;
   double value;
@@ -231,6 +259,7 @@ struct ScoreArgs {
   const Coef *coef;          // [2*P][kcap]
   const Coef32 *coef32;      // [2*P][kcap / kCoefBlock] block-local fp32 LSE terms
   const CoefM *coefm;        // [2*P][mom_stride] moment form of 16-component chunks
+  const CoefM8 *coefm8;      // [2*P][kcap / kCoefBlock] moment form of 8-component blocks
   const double *mw, *mmu, *msig;  // [2*P][kcap] (sampler reads side 0)
   const uint64_t *seeds;     // [S]
   const double *cand;        // candidates [S][n_slots][n_cand] (drawn or external)
@@ -271,7 +300,8 @@ struct ScoreArgs {
   int32_t lse_f32;           // unpruned log-sum-exp slots also take the block-local fp32
                              // pairs (prune mode 3's arithmetic on small draws)
   int32_t lse_mom;           // prune mode 3 wave tiles take the moment form of eligible
-                             // 16-component chunks (CoefM; TPE_MOMENT=0 switches it off)
+                             // chunks: 16 (CoefM), 8 (CoefM8, blocks) or 0 (TPE_MOMENT=0,
+                             // or no table written by the last fit)
   int32_t lookup_draw;       // the sorted draw leaves the lookup slots (categorical, value
                              // lattice) unwritten and the scoring tile draws them itself,
                              // for below mixtures of 1 .. kFuseTab components (lookup_inline)
@@ -309,7 +339,8 @@ struct FitArgs {
   MixInfo *info;             // [2P]
   Coef *coef;                // [2P][kcap]
   Coef32 *coef32;            // [2P][kcap / kCoefBlock]
-  CoefM *coefm;              // [2P][mom_stride(kcap)]
+  CoefM *coefm;              // [2P][mom_stride(kcap)] (null: not written)
+  CoefM8 *coefm8;            // [2P][kcap / kCoefBlock] (null: not written; at most one of the two)
   int64_t kcap;
   double *ob;                // [2P][kcap] scratch: observations of the slot
   double *tmp;               // [2P][kcap] scratch (may alias ob)
@@ -331,8 +362,8 @@ bool is_sorted_draw_kernel_fn(const void *f);
 const void *lattice_draw_kernel_fn();      // k_lattice<true> (lattice + fused draw)
 hipError_t launch_prep(const tpe_hp *hps, int32_t n_hp, const double *mw,
                        const double *mmu, const double *msig, MixInfo *info,
-                       Coef *coef, Coef32 *coef32, CoefM *coefm, int64_t kcap, double *scratch,
-                       hipStream_t st);
+                       Coef *coef, Coef32 *coef32, CoefM *coefm, CoefM8 *coefm8, int64_t kcap,
+                       double *scratch, hipStream_t st);
 // a level mixing wave-tile log-sum-exp groups with other kinds runs two
 // launches: the other kinds on `side` between fork / join events (when side
 // is given; st waits for the join), the log-sum-exp groups on st

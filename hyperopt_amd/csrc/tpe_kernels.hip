@@ -544,6 +544,50 @@ __global__ __launch_bounds__(256) void k_micro(int iters, double *sink) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) acc += sm[c];
     if (acc == 12345.0) sink[t] = acc;
+  } else if constexpr (WHICH == 9) {
+    // the 8-wide moment form (CoefM8): per (candidate row pair, block of 8)
+    // the same steps as WHICH 8 with a degree-kMom8Deg polynomial; 2 row
+    // pairs x 2 blocks = 4 x 2 x 8 pairs
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    double y[4], sm[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) { y[c] = 1e-3 * (t + c); sm[c] = 0.0; }
+    float mm[2][kMom8Deg + 1];
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int q = 0; q <= kMom8Deg; ++q) mm[b][q] = 1.0f / (1.0f + q + b);
+    const double centre[2] = {0.25, 0.75};
+    float A = 3.0f;
+    const float Mf = 5.0f, gam = -72.0f;
+    for (int i = 0; i < iters; ++i) {
+      const float off = 0.5f + (A - Mf);
+#pragma unroll
+      for (int c = 0; c < 4; c += 2) {
+        float bs[2][2];
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const f2v v = {(float)(y[c] - centre[b]), (float)(y[c + 1] - centre[b])};
+          const f2v arg = __builtin_elementwise_fma(f2v{gam, gam}, v * v, f2v{off, off});
+          f2v p = __builtin_elementwise_fma(f2v{mm[b][kMom8Deg], mm[b][kMom8Deg]}, v,
+                                            f2v{mm[b][kMom8Deg - 1], mm[b][kMom8Deg - 1]});
+#pragma unroll
+          for (int q = kMom8Deg - 2; q >= 0; --q)
+            p = __builtin_elementwise_fma(p, v, f2v{mm[b][q], mm[b][q]});
+          bs[b][0] = __builtin_amdgcn_exp2f(arg.x) * p.x;
+          bs[b][1] = __builtin_amdgcn_exp2f(arg.y) * p.y;
+        }
+        sm[c] += (double)(bs[0][0] + bs[1][0]);
+        sm[c + 1] += (double)(bs[0][1] + bs[1][1]);
+        y[c] += 1e-9;
+        y[c + 1] += 1e-9;
+      }
+      A += 1e-7f;
+    }
+    double acc = 0.0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc += sm[c];
+    if (acc == 12345.0) sink[t] = acc;
   } else if constexpr (WHICH == 4) {
     // one quantized pair exactly as k_score computes a live one: two OCML
     // fp64 erf, the reference's Phi and two-stage increment; 2 chains
@@ -591,6 +635,7 @@ hipError_t launch_micro(int which, int blocks, int iters, double *sink, hipStrea
     case 6: k_micro<6><<<blocks, 256, 0, st>>>(iters, sink); break;
     case 7: k_micro<7><<<blocks, 256, 0, st>>>(iters, sink); break;
     case 8: k_micro<8><<<blocks, 256, 0, st>>>(iters, sink); break;
+    case 9: k_micro<9><<<blocks, 256, 0, st>>>(iters, sink); break;
     default: k_micro<2><<<blocks, 256, 0, st>>>(iters, sink); break;
   }
   return hipGetLastError();

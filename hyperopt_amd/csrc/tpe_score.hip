@@ -194,6 +194,51 @@ __device__ __forceinline__ void mom_sum(const f2v &arg, const f2v &p, float (&bs
   bs[0] = __builtin_amdgcn_exp2f(arg.x) * p.x;
   bs[1] = __builtin_amdgcn_exp2f(arg.y) * p.y;
 }
+// The 8-wide moment form (CoefM8, one coefficient block, degree kMom8Deg):
+// the same arithmetic with 16 coefficients; one entry = two 64-B scalar loads
+typedef const CoefM8 __attribute__((address_space(4))) KCM8;
+__device__ __forceinline__ KCM8 *uniform_ptrm8(const CoefM8 *p) {
+  const uint64_t u = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  return (KCM8 *)(((uint64_t)hi << 32) | lo);
+}
+struct Mom8Group {
+  double c;
+  float A, cm, g;
+  float m[kMom8Deg + 1];
+};
+__device__ __forceinline__ void load_mom8(KCM8 *__restrict__ rb, uint32_t j, Mom8Group &g) {
+  KCM8 *b = rb + j;
+  g.c = b->center;
+  g.A = b->base;
+  g.cm = b->cm;
+  g.g = b->gam;
+#pragma unroll
+  for (int q = 0; q <= kMom8Deg; ++q) g.m[q] = b->m[q];
+}
+// two candidate rows of a lane against one block
+__device__ __forceinline__ void mom8_terms(const Mom8Group &g, float Mf, const double (&y)[2],
+                                           f2v &arg, f2v &p) {
+  const float off = g.cm + (g.A - Mf);
+  const f2v v = {(float)(y[0] - g.c), (float)(y[1] - g.c)};
+  arg = __builtin_elementwise_fma(f2v{g.g, g.g}, v * v, f2v{off, off});
+  p = __builtin_elementwise_fma(f2v{g.m[kMom8Deg], g.m[kMom8Deg]}, v,
+                                f2v{g.m[kMom8Deg - 1], g.m[kMom8Deg - 1]});
+#pragma unroll
+  for (int q = kMom8Deg - 2; q >= 0; --q) p = __builtin_elementwise_fma(p, v, f2v{g.m[q], g.m[q]});
+}
+// one candidate row against two blocks a, b packed
+__device__ __forceinline__ void mom8_terms2(const Mom8Group &a, const Mom8Group &b, float Mf,
+                                            double y, f2v &arg, f2v &p) {
+  const f2v off = {a.cm + (a.A - Mf), b.cm + (b.A - Mf)};
+  const f2v v = {(float)(y - a.c), (float)(y - b.c)};
+  arg = __builtin_elementwise_fma(f2v{a.g, b.g}, v * v, off);
+  p = __builtin_elementwise_fma(f2v{a.m[kMom8Deg], b.m[kMom8Deg]}, v,
+                                f2v{a.m[kMom8Deg - 1], b.m[kMom8Deg - 1]});
+#pragma unroll
+  for (int q = kMom8Deg - 2; q >= 0; --q) p = __builtin_elementwise_fma(p, v, f2v{a.m[q], b.m[q]});
+}
 
 // Tables staged in LDS (the one-row wave-tile kernel, k_score_wave1): a
 // mixture's block envelopes and block-local fp32 blocks copied once per
@@ -337,7 +382,8 @@ struct LseCensus {
   uint32_t f32;                 // the evaluated ones in the fp32 per-group-lift form
   uint32_t retry;               // one-exponent pairs evaluated again by a second attempt
   uint32_t wide;                // one-exponent pairs of wide blocks (fp64 loop, mode 3)
-  uint32_t mom;                 // one-exponent pairs evaluated in the moment form (CoefM)
+  uint32_t mom;                 // one-exponent pairs evaluated in the moment form (CoefM / CoefM8)
+  uint32_t mom8;                // of those, in the 8-wide form (CoefM8)
 };
 
 // A block's envelope bound over the wave's candidate range [lo, hi]: the
@@ -593,13 +639,16 @@ __device__ __forceinline__ void lse_terms_f32(const CoefGroup32 &g, float Mf,
   }
 }
 
-template <int KR, bool CENSUS, int STRIDE = kWaves, bool F32 = false, bool STG = false>
+// MW: the moment width of the launch (16: CoefM chunks in cmv, 8: CoefM8
+// blocks in cmv8; the kernels are instantiated per width, tpe_internal.hpp)
+template <int KR, bool CENSUS, int STRIDE = kWaves, bool F32 = false, bool STG = false, int MW = 16>
 __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
                                                    const Coef *__restrict__ cv, int c0, int nb,
                                                    const double (&y)[KR], const bool (&valid)[KR],
                                                    LseAcc (&out)[KR], LseWindow win, int nvalid,
                                                    LseCensus &cen, KC32 *__restrict__ c32 = nullptr,
                                                    const CoefM *__restrict__ cmv = nullptr,
+                                                   const CoefM8 *__restrict__ cmv8 = nullptr,
                                                    Stage stg = {}) {
   const int lane = threadIdx.x & 63;
   const int nch = (nb + kChunk - 1) / kChunk;
@@ -759,34 +808,104 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
         // log2 tau + bound <= thr + 1, i.e. tau 2^(bound - L) <= 2^-dead, the
         // skipped blocks' budget per component -- far chunks of a wide halo
         // qualify at larger x -- and x <= kMomXCap (fp32 Horner conditioning
-        // e^(2x) bounded)
-        const float bnd1 = __builtin_bit_cast(float, dpp<kDppXor1>(__builtin_bit_cast(int, bnd)));
-        bool elig = false;
-        if (KR <= 2 && cmv && has && !(lane & 1)) {
-          const CoefM *q = cmv + (r0 + (lane >> 1));
-          const float cf = (float)q->center;
-          const float x = fmaxf(fabsf(win.lo - cf), fabsf(win.hi - cf)) * q->xh;
-          const float l2tau = (float)(kMomDeg + 1) * __builtin_amdgcn_logf(x) +
-                              x * 1.44269504f - kMomLog2Fact;
-          elig = x <= kMomXLim || (x <= kMomXCap && l2tau + fmaxf(bnd, bnd1) <= win.thr + 1.0f);
+        // e^(2x) bounded).  8-wide (MW 8): lane l tests its own block (one
+        // CoefM8 entry per block, degree kMom8Deg), the chunk is the block.
+        uint64_t cmask = 0;
+        if constexpr (MW == 8) {
+          bool elig = false;
+          if (KR <= 2 && cmv8 && has) {
+            const CoefM8 *q = cmv8 + (2 * r0 + lane);
+            const float cf = (float)q->center;
+            const float x = fmaxf(fabsf(win.lo - cf), fabsf(win.hi - cf)) * q->xh;
+            const float l2tau = (float)(kMom8Deg + 1) * __builtin_amdgcn_logf(x) +
+                                x * 1.44269504f - kMom8Log2Fact;
+            elig = x <= kMomXLim || (x <= kMomXCap && l2tau + bnd <= win.thr + 1.0f);
+          }
+          cmask = __ballot(live && elig);
+        } else {
+          const float bnd1 = __builtin_bit_cast(float, dpp<kDppXor1>(__builtin_bit_cast(int, bnd)));
+          bool elig = false;
+          if (KR <= 2 && cmv && has && !(lane & 1)) {
+            const CoefM *q = cmv + (r0 + (lane >> 1));
+            const float cf = (float)q->center;
+            const float x = fmaxf(fabsf(win.lo - cf), fabsf(win.hi - cf)) * q->xh;
+            const float l2tau = (float)(kMomDeg + 1) * __builtin_amdgcn_logf(x) +
+                                x * 1.44269504f - kMomLog2Fact;
+            elig = x <= kMomXLim || (x <= kMomXCap && l2tau + fmaxf(bnd, bnd1) <= win.thr + 1.0f);
+          }
+          const uint64_t lm = __ballot(live);
+          cmask = (lm | (lm >> 1)) & __ballot(elig) & kEven;
         }
-        const uint64_t lm = __ballot(live);
-        const uint64_t cmask = (lm | (lm >> 1)) & __ballot(elig) & kEven;
-        const uint64_t cover = cmask | (cmask << 1);
+        const uint64_t cover = MW == 8 ? cmask : cmask | (cmask << 1);
         if constexpr (CENSUS) {
-          const int n = (cmask >> lane) & 1 ? min(kMomChunk, nb - k0) : 0;
+          const int n = (cmask >> lane) & 1 ? min(MW == 8 ? kGroup : kMomChunk, nb - k0) : 0;
           uint32_t mx = (uint32_t)n;
 #pragma unroll
           for (int o = 32; o > 0; o >>= 1) mx += __shfl_xor(mx, o, 64);
-          // (the chunk's blocks counted as evaluated whether or not both were live)
-          uint32_t lx = (uint32_t)(has && (((cover & ~lm) >> lane) & 1) ? min(kGroup, nb - k0) : 0);
-#pragma unroll
-          for (int o = 32; o > 0; o >>= 1) lx += __shfl_xor(lx, o, 64);
           cen.mom += mx * (uint32_t)nvalid;
-          cen.exec += lx * (uint32_t)nvalid;
-          cen.shift += lx * (uint32_t)nvalid;
+          if (MW == 8) cen.mom8 += mx * (uint32_t)nvalid;
+          if constexpr (MW != 8) {
+            // (the chunk's blocks counted as evaluated whether or not both were live)
+            const uint64_t lm = __ballot(live);
+            uint32_t lx = (uint32_t)(has && (((cover & ~lm) >> lane) & 1) ? min(kGroup, nb - k0) : 0);
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) lx += __shfl_xor(lx, o, 64);
+            cen.exec += lx * (uint32_t)nvalid;
+            cen.shift += lx * (uint32_t)nvalid;
+          }
         }
-        if constexpr (KR == 2) {
+        if constexpr (MW == 8 && KR == 2) {
+          KCM8 *rm = uniform_ptrm8(cmv8) + 2 * r0;
+          uint64_t cm = cmask;
+          bool hm = cm != 0;
+          Mom8Group g;
+          if (hm) load_mom8(rm, low_bit(cm), g);
+          // two blocks per iteration, their fp32 sums added in fp32 and
+          // converted once (as the pair loop below)
+          while (hm) {
+            f2v a0, p0;
+            mom8_terms(g, Mf, y, a0, p0);
+            cm &= cm - 1;
+            hm = cm != 0;
+            load_mom8(rm, low_bit(cm), g);
+            __builtin_amdgcn_sched_barrier(0);
+            float b0[2];
+            mom_sum(a0, p0, b0);
+            if (!hm) {
+#pragma unroll
+              for (int r = 0; r < KR; ++r) s[r] += (double)b0[r];
+              break;
+            }
+            f2v a1, p1;
+            mom8_terms(g, Mf, y, a1, p1);
+            cm &= cm - 1;
+            hm = cm != 0;
+            load_mom8(rm, low_bit(cm), g);
+            __builtin_amdgcn_sched_barrier(0);
+            float b1[2];
+            mom_sum(a1, p1, b1);
+#pragma unroll
+            for (int r = 0; r < KR; ++r) s[r] += (double)(b0[r] + b1[r]);
+          }
+        } else if constexpr (MW == 8 && KR == 1) {
+          // one row: blocks in pairs (the second of an odd last pair is block
+          // 0 of the round again, a valid address, its sum dropped)
+          KCM8 *rm = uniform_ptrm8(cmv8) + 2 * r0;
+          uint64_t cm = cmask;
+          while (cm) {
+            Mom8Group ga, gb;
+            load_mom8(rm, low_bit(cm), ga);
+            cm &= cm - 1;
+            const bool two = cm != 0;
+            load_mom8(rm, low_bit(cm), gb);
+            cm &= cm - 1;
+            f2v a2, p2;
+            mom8_terms2(ga, gb, Mf, y[0], a2, p2);
+            float b2[2];
+            mom_sum(a2, p2, b2);
+            s[0] += (double)(two ? b2[0] + b2[1] : b2[0]);
+          }
+        } else if constexpr (KR == 2) {
           KCM *rm = uniform_ptrm(cmv) + r0;
           uint64_t cm = cmask;
           bool hm = cm != 0;
@@ -1264,7 +1383,7 @@ __device__ __forceinline__ void publish_arrive(const ScoreArgs &A) {
 
 // (SM: ScoreSmem, or ScoreSmem1 for the one-row wave tiles, whose
 // workgroup stages both mixtures' tables in LDS when they fit kStageBlocks)
-template <int KIND, bool CENSUS, typename SM, bool LDRAW = false, bool TDRAW = false>
+template <int KIND, bool CENSUS, typename SM, bool LDRAW = false, bool TDRAW = false, int MW = 16>
 __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot, int tile,
                                            int ntiles, bool known_active) {
   constexpr bool STAGE = std::is_same<SM, ScoreSmem1>::value;
@@ -1417,21 +1536,10 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
     li[r] = wt0 + r * 64 + lane;
     valid[r] = li[r] < A.n_cand;
     if constexpr (LDRAW && (LAT || KIND == KIND_CAT)) {
-      x[r] = 0.0;  // (the scan below draws its own)
+      // (self-drawing lookups: the scan in the finalize below, lookup_scan,
+      // draws and scores its own candidates; nothing is read here)
+      x[r] = 0.0;
       continue;
-      if (ldraw) {
-        const uint64_t gi = (uint64_t)(A.cand_begin + li[r]);
-        const uint64_t seed = suggestion_seed(A, s);
-        // (out of line, as in the draw kernels: inlined, its inverse CDFs
-        // would set the register allocation of the whole scoring kernel)
-        x[r] = valid[r] ? draw_table_ool<kFuseTab>(A.hps + hp, ib.K, A.mmu + sb * A.kcap,
-                                                   A.msig + sb * A.kcap, &sm.dt,
-                                                   draw_block0(seed, gi, (uint32_t)hp), seed, gi,
-                                                   (uint32_t)hp)
-                        : 0.0;
-      } else {
-        x[r] = valid[r] ? cand[li[r]] : 0.0;
-      }
     } else if constexpr (TDRAW) {
       const uint64_t gi = (uint64_t)(A.cand_begin + li[r]);
       const uint64_t seed = suggestion_seed(A, s);
@@ -1498,7 +1606,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
     // wave index as a scalar: the component addresses below are wave-uniform,
     // so the coefficients come in through scalar loads (SGPR operands)
     const int wv = __builtin_amdgcn_readfirstlane(wave);
-    LseCensus lcen{0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    LseCensus lcen{0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
     int nvalid = 0;
 #pragma unroll
     for (int r = 0; r < KR; ++r) nvalid += valid[r] ? 1 : 0;
@@ -1543,16 +1651,20 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
           stv.c32 = (LC32 *)(sm.stg.c32 + (mix ? nbb : 0));
         }
         if (prune && A.lse_prune > 1 && K >= A.lse_shift_min && win.thr > -INFINITY) {
+          // (the moment table of the launch's width: CoefM chunks or CoefM8 blocks)
+          const int64_t ms = mix ? sa : sb;
+          const CoefM *mt16 =
+              (MW == 16 && A.lse_mom == 16) ? A.coefm + ms * mom_stride(A.kcap) : nullptr;
+          const CoefM8 *mt8 =
+              (MW == 8 && A.lse_mom == 8) ? A.coefm8 + ms * (A.kcap / kCoefBlock) : nullptr;
           if (STAGE && staged)  // (prune mode 3 only: the staged blocks are Coef32)
-            shifted = lse_chunks_shifted<KR, CENSUS, ST, true, STAGE>(
+            shifted = lse_chunks_shifted<KR, CENSUS, ST, true, STAGE, MW>(
                 uniform_ptr(cm), cm, cw0, K, y, valid, lacc[mix], win, nvalid, lcen,
-                uniform_ptr32(A.coef32 + (mix ? sa : sb) * (A.kcap / kCoefBlock)),
-                A.lse_mom ? A.coefm + (mix ? sa : sb) * mom_stride(A.kcap) : nullptr, stv);
-          else if (A.lse_prune > 2)  // block-local fp32 pairs (Coef32), moment chunks (CoefM)
-            shifted = lse_chunks_shifted<KR, CENSUS, ST, true>(
+                uniform_ptr32(A.coef32 + ms * (A.kcap / kCoefBlock)), mt16, mt8, stv);
+          else if (A.lse_prune > 2)  // block-local fp32 pairs (Coef32), moment chunks (CoefM / 8)
+            shifted = lse_chunks_shifted<KR, CENSUS, ST, true, false, MW>(
                 uniform_ptr(cm), cm, cw0, K, y, valid, lacc[mix], win, nvalid, lcen,
-                uniform_ptr32(A.coef32 + (mix ? sa : sb) * (A.kcap / kCoefBlock)),
-                A.lse_mom ? A.coefm + (mix ? sa : sb) * mom_stride(A.kcap) : nullptr);
+                uniform_ptr32(A.coef32 + ms * (A.kcap / kCoefBlock)), mt16, mt8);
           else
             shifted = lse_chunks_shifted<KR, CENSUS, ST>(uniform_ptr(cm), cm, cw0, K, y, valid,
                                                          lacc[mix], win, nvalid, lcen);
@@ -1612,10 +1724,10 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
     }
     if constexpr (CENSUS && LSE) {
       // nvalid is per lane: the per-lane sums add up to the wave's pairs
-      unsigned long long c2[7] = {lcen.total, lcen.exec, lcen.shift, lcen.f32, lcen.retry,
-                                  lcen.wide, lcen.mom};
+      unsigned long long c2[8] = {lcen.total, lcen.exec, lcen.shift, lcen.f32, lcen.retry,
+                                  lcen.wide, lcen.mom, lcen.mom8};
 #pragma unroll
-      for (int q = 0; q < 7; ++q) {
+      for (int q = 0; q < 8; ++q) {
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) c2[q] += __shfl_xor(c2[q], o, 64);
       }
@@ -1627,6 +1739,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
         atomicAdd(A.census + 7, c2[4]);
         atomicAdd(A.census + 8, c2[5]);
         atomicAdd(A.census + 9, c2[6]);
+        atomicAdd(A.census + 10, c2[7]);
       }
     }
     if constexpr (!WT) {
@@ -2039,7 +2152,7 @@ __device__ __forceinline__ void mark_inactive(const ScoreArgs &A, int s, int s0,
 // allocation -- the combined one keeps the most any kind needs).
 enum { kSetNoErf = 0, kSetAll = 1, kSetWave = 2, kSetWave1 = 3, kSetLookup = 4, kSetTiny = 5 };
 
-template <int SET, bool CENSUS, typename SM>
+template <int SET, bool CENSUS, typename SM, int MW = 16>
 __device__ __forceinline__ void score_block(const ScoreArgs &A, SM &sm) {
   const int b = blockIdx.x;
   int g = 0;
@@ -2057,8 +2170,9 @@ __device__ __forceinline__ void score_block(const ScoreArgs &A, SM &sm) {
   }
   const bool known = A.compact != 0;
   if constexpr (SET == kSetWave) {
-    if (A.grp_kind[g] == KIND_LSE_LW) score_tile<KIND_LSE_LW, CENSUS, SM>(A, sm, slot, tile, nt, known);
-    else score_tile<KIND_LSE_GW, CENSUS, SM>(A, sm, slot, tile, nt, known);
+    if (A.grp_kind[g] == KIND_LSE_LW)
+      score_tile<KIND_LSE_LW, CENSUS, SM, false, false, MW>(A, sm, slot, tile, nt, known);
+    else score_tile<KIND_LSE_GW, CENSUS, SM, false, false, MW>(A, sm, slot, tile, nt, known);
     return;
   } else if constexpr (SET == kSetLookup) {
     if (A.grp_kind[g] == KIND_LAT) score_tile<KIND_LAT, CENSUS, SM, true>(A, sm, slot, tile, nt, known);
@@ -2076,8 +2190,9 @@ __device__ __forceinline__ void score_block(const ScoreArgs &A, SM &sm) {
     }
     return;
   } else if constexpr (SET == kSetWave1) {
-    if (A.grp_kind[g] == KIND_LSE_LW1) score_tile<KIND_LSE_LW1, CENSUS, SM>(A, sm, slot, tile, nt, known);
-    else score_tile<KIND_LSE_GW1, CENSUS, SM>(A, sm, slot, tile, nt, known);
+    if (A.grp_kind[g] == KIND_LSE_LW1)
+      score_tile<KIND_LSE_LW1, CENSUS, SM, false, false, MW>(A, sm, slot, tile, nt, known);
+    else score_tile<KIND_LSE_GW1, CENSUS, SM, false, false, MW>(A, sm, slot, tile, nt, known);
     return;
   } else {
     switch (A.grp_kind[g]) {
@@ -2109,19 +2224,22 @@ void k_score(ScoreArgs A) {
 #ifndef TPE_WAVE_EU
 #define TPE_WAVE_EU 6
 #endif
-template <bool CENSUS>
+// MW: the moment width (16: CoefM chunks, the config-4 regime; 8: CoefM8
+// blocks, mixtures of ~1e3 components) -- one instantiation per width, so
+// each keeps its own register allocation
+template <bool CENSUS, int MW>
 __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(TPE_WAVE_EU)))
 void k_score_wave(ScoreArgs A) {
   __shared__ ScoreSmem sm;
-  score_block<kSetWave, CENSUS>(A, sm);
+  score_block<kSetWave, CENSUS, ScoreSmem, MW>(A, sm);
 }
 // the one-row wave tiles (KIND_LSE_GW1 / LW1) in a kernel of their own: the
 // two-row kernel's register allocation is left as it is
-template <bool CENSUS>
+template <bool CENSUS, int MW>
 __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(TPE_WAVE_EU)))
 void k_score_wave1(ScoreArgs A) {
   __shared__ ScoreSmem1 sm;
-  score_block<kSetWave1, CENSUS>(A, sm);
+  score_block<kSetWave1, CENSUS, ScoreSmem1, MW>(A, sm);
 }
 
 // tiny unsorted draws whose tiles draw their own candidates (tile_draw), in a
@@ -2385,12 +2503,23 @@ static hipError_t launch_class(const ScoreArgs &a, int cls, bool has_erf, hipStr
   bool one_row = false;
   for (int i = 0; i < a.n_groups; ++i)
     one_row |= a.grp_kind[i] == KIND_LSE_GW1 || a.grp_kind[i] == KIND_LSE_LW1;
+  const bool m8 = a.lse_mom == 8;
   if (cls == 0 && one_row) {
-    if (a.census) k_score_wave1<true><<<g, kWaves * 64, 0, st>>>(a);
-    else k_score_wave1<false><<<g, kWaves * 64, 0, st>>>(a);
+    if (m8) {
+      if (a.census) k_score_wave1<true, 8><<<g, kWaves * 64, 0, st>>>(a);
+      else k_score_wave1<false, 8><<<g, kWaves * 64, 0, st>>>(a);
+    } else {
+      if (a.census) k_score_wave1<true, 16><<<g, kWaves * 64, 0, st>>>(a);
+      else k_score_wave1<false, 16><<<g, kWaves * 64, 0, st>>>(a);
+    }
   } else if (cls == 0) {
-    if (a.census) k_score_wave<true><<<g, kWaves * 64, 0, st>>>(a);
-    else k_score_wave<false><<<g, kWaves * 64, 0, st>>>(a);
+    if (m8) {
+      if (a.census) k_score_wave<true, 8><<<g, kWaves * 64, 0, st>>>(a);
+      else k_score_wave<false, 8><<<g, kWaves * 64, 0, st>>>(a);
+    } else {
+      if (a.census) k_score_wave<true, 16><<<g, kWaves * 64, 0, st>>>(a);
+      else k_score_wave<false, 16><<<g, kWaves * 64, 0, st>>>(a);
+    }
   } else if (cls == 1) {
     // one block per segment of a slot (the scan's early exit works within a
     // segment) instead of one per 2048-candidate tile: segments of whole

@@ -193,7 +193,9 @@ int tpe_plan_get_mixture(tpe_plan_t p, int32_t hp, int32_t side, double *w,
  * side) as written by the last fit -- which 0: the per-component coefficient
  * table (32 B per component, field-major blocks of 8, envelopes in the
  * w-rows), 1: the block-local fp32 table (128 B per block of 8), 2: the
- * moment table of 16-component chunks (64 B each).  *bytes = the table's
+ * moment table of 16-component chunks (64 B each), 3: the 8-wide moment
+ * table (128 B per block of 8; written instead of 2 for mixtures of ~1e3
+ * components, the other one is then stale).  *bytes = the table's
  * size; out may be NULL (size query).  The layouts are internal
  * (tpe_internal.hpp) and may change between versions.                      */
 int tpe_plan_get_table(tpe_plan_t p, int32_t hp, int32_t side, int32_t which, void *out,
@@ -295,13 +297,14 @@ int tpe_plan_set_lattice(tpe_plan_t p, int32_t enable);
  * zeros; a wave's retried pass counts again) -- and switch the census on (enable != 0)
  * or off for the following suggests.  counts has 6 entries.               */
 int tpe_plan_census(tpe_plan_t p, int32_t enable, int64_t *counts);
-/* The same with n_counts entries (up to 10): [6] of [5] the log-sum-exp pairs
+/* The same with n_counts entries (up to 11): [6] of [5] the log-sum-exp pairs
  * evaluated in the block-local fp32 per-group-lift form (prune mode 3 on
  * mixtures below the one-exponent size), [7] of [4] the one-exponent pairs
  * evaluated again by a wave's second attempt (its exponent re-centred),
  * [8] of [4] the one-exponent pairs of wide blocks (mode 3's fp64 loop),
  * [9] of [4] the one-exponent pairs evaluated in the moment form of their
- * 16-component chunk (one exp2 + a degree-9 polynomial per chunk).         */
+ * 16-component chunk (one exp2 + a degree-9 polynomial per chunk) or, [10]
+ * of [9], of their 8-component block (one exp2 + a degree-15 polynomial). */
 int tpe_plan_census_n(tpe_plan_t p, int32_t enable, int64_t *counts, int32_t n_counts);
 
 /* Prior draws of n_suggest whole suggestions (rand.suggest, the TPE startup
@@ -334,7 +337,9 @@ int tpe_plan_set_prune(tpe_plan_t p, int32_t mode);
  * same pair in block-local fp32 (mode 3; pairs/s), 7 the per-group-lift pair
  * in block-local fp32 (mode 3 below the one-exponent size; pairs/s), 8 the
  * moment form of a 16-component chunk (one exp2 + a degree-9 polynomial per
- * candidate and chunk; pairs/s, 16 per chunk evaluation).                   */
+ * candidate and chunk; pairs/s, 16 per chunk evaluation), 9 the 8-wide moment
+ * form (one exp2 + a degree-15 polynomial per candidate and block of 8;
+ * pairs/s, 8 per block evaluation).                                         */
 int tpe_microbench(tpe_handle_t h, int32_t which, double *per_second);
 
 #ifdef __cplusplus

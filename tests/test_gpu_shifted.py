@@ -678,3 +678,120 @@ def test_moment_table_vs_numpy(cfg4_plan):
                 np.testing.assert_allclose(e['m'], mom, rtol=2e-7, atol=1e-30)
             if side == 1:
                 assert n_ok >= 0.99 * (-(-K // 16)) - 1, (lab, n_ok)
+
+
+_MOM8 = np.dtype([('center', '<f8'), ('xh', '<f4'), ('base', '<f4'), ('cm', '<f4'), ('gam', '<f4'),
+                  ('m', '<f4', (16,)), ('pad', '<f4', (10,))])
+
+
+def test_moment8_table_vs_numpy():
+    """The 8-wide moment table (CoefM8, tpe_plan_get_table which=3) the fit
+    writes for config 2's mixtures (N = 1e3: K_a = 993, mom_width 8) against
+    a float64 numpy restatement of the plan's own fitted mixture: per block of
+    8 mu-sorted components, centre = mu' midpoint, T_k = c_k - a^2 d_k^2,
+    m_j = sum_k 2^(T_k - T*) q_k^j / j! (j <= 15), q_k = 2 a^2 ln2 d_k,
+    xh = max |q_k|; blocks whose sigmas differ (the prior's) are not
+    eligible (xh = +inf).  fp32 fields to fp32 rounding."""
+    import bench
+    from oracle import tpe_oracle as O
+    assert _MOM8.itemsize == 128
+    dom, losses, vals, act = bench.build_workload('cfg2')
+    hps, conds, pprior = dom.space.engine_tables()
+    plan = E.Plan(E.default_engine(), hps, conds, pprior, max_trials=losses.size)
+    plan.set_history(losses, vals, act)
+    plan.fit()
+    LOG2E, LN2 = 1.4426950408889634, math.log(2.0)
+    for lab in ('u0', 'u3'):
+        hp_i = dom.space.by_label[lab].index
+        t_pm = hps[hp_i].prior_mu
+        for side in (0, 1):
+            w, mu, sg = plan.mixture(hp_i, side)
+            t = plan.table(hp_i, side, 3).view(_MOM8)
+            K = w.size
+            sgc = np.maximum(sg, 1e-12)
+            pacc = np.sum(w * (O.normal_cdf(5.0, mu, sgc) - O.normal_cdf(-5.0, mu, sgc)))
+            c = LOG2E * np.log(w / np.sqrt(2 * np.pi * sgc ** 2) / pacc)
+            a2 = LOG2E / (2 * sgc ** 2)
+            n_ok = 0
+            for b in range(-(-K // 8)):
+                sl = slice(8 * b, min(K, 8 * b + 8))
+                m_, a2_, c_ = mu[sl] - t_pm, a2[sl], c[sl]
+                e = t[b]
+                if not np.all(a2_ == a2_[0]):
+                    assert np.isinf(e['xh']), (lab, side, b)
+                    continue
+                n_ok += 1
+                cen = 0.5 * (m_.min() + m_.max())
+                d = m_ - cen
+                T = c_ - a2_ * d * d
+                Ts = T.max()
+                rho = np.exp2(T - Ts)
+                q = 2 * a2_[0] * LN2 * d
+                mom = np.array([np.sum(rho * q ** j) / math.factorial(j) for j in range(16)])
+                assert e['center'] == cen, (lab, side, b)
+                np.testing.assert_allclose(e['xh'], np.abs(q).max(), rtol=2e-7)   # (rounded up)
+                assert e['base'] == np.floor(Ts)
+                np.testing.assert_allclose(e['cm'], Ts - np.floor(Ts), atol=2e-7)
+                np.testing.assert_allclose(e['gam'], -a2_[0], rtol=1e-7)
+                np.testing.assert_allclose(e['m'], mom, rtol=2e-7, atol=1e-30)
+            if side == 1:
+                assert K > 900 and n_ok >= 0.99 * (-(-K // 8)) - 1, (lab, n_ok)
+
+
+def test_config5_moment8_census():
+    """Config 5's shape (config 2's space and history, K_a = 993, 1e6
+    candidates per suggestion, two-row wave tiles) scores most of its
+    evaluated log-sum-exp pairs in the 8-wide moment form (census [10]), and
+    config 3's one-row tiles (1e5 candidates, K_a ~ 1.4e3) take it too."""
+    import bench
+    for cfg, n, frac in (('cfg2', 1_000_000, 0.5), ('cfg3', 100_000, 0.3)):
+        dom, losses, vals, act = bench.build_workload(cfg)
+        hps, conds, pprior = dom.space.engine_tables()
+        plan = E.Plan(E.default_engine(), hps, conds, pprior, max_trials=losses.size)
+        plan.set_history(losses, vals, act)
+        plan.census(True)
+        plan.fit_suggest([1234567], n)
+        census = plan.census(False, n=11)
+        assert census[10] == census[9] > frac * census[5], (cfg, census)
+        _record('moment8_census_%s' % cfg, census=list(census))
+
+
+def test_lookup_scan_edge_lattice_points():
+    """The self-drawing lookup scan's early exit (k_score_lookup) stops at the
+    slot's best reachable lattice score, which leaves out the lattice's margin
+    points: bounded quantized GMM / LGMM hps whose bounds are exact multiples
+    of q and whose best value is an edge point of the lattice (the history's
+    good trials sit at the bounds), on sorted draws of 2^21 candidates: the
+    early-exit records equal the drawn-and-read full scan's
+    (TPE_LOOKUP_DRAW=0) byte for byte, and the winners are edge values."""
+    code = """
+import sys, math, numpy as np
+sys.path.insert(0, 'tests')
+from hyperopt_amd import hp, rand, Trials, _engine as E
+from hyperopt_amd.base import Domain
+from hyperopt_amd.tpe import build_history
+space = {'a': hp.quniform('a', 0, 10, 1), 'b': hp.qloguniform('b', 0, math.log(64), 1),
+         'c': hp.quniform('c', -4, 4, 2)}
+dom = Domain(lambda x: 0.0, space)
+t = Trials()
+docs = rand.suggest(list(range(400)), dom, t, 3)
+edge = {'a': 10.0, 'b': 64.0, 'c': 4.0}
+for d in docs:
+    v = {k: d['misc']['vals'][k][0] for k in edge}
+    d['state'] = 2
+    d['result'] = {'status': 'ok', 'loss': float(sum(abs(v[k] - edge[k]) / (1 + abs(edge[k])) for k in edge))}
+t._insert_trial_docs(docs)
+t.refresh()
+_, losses, vals, act = build_history(dom, t, dom.space.labels)
+hps, conds, pprior = dom.space.engine_tables()
+plan = E.Plan(E.default_engine(), hps, conds, pprior, max_trials=losses.size)
+plan.set_history(losses, vals, act)
+res = plan.fit_suggest([99, 100], 1 << 21)
+print('vals', sorted((l, float(res[0]['value'][dom.space.by_label[l].index])) for l in edge))
+print('hex', res.view(np.uint8).tobytes().hex())
+"""
+    a = _child(code, {})
+    b = _child(code, {'TPE_LOOKUP_DRAW': '0'})
+    assert a.split('hex ')[1].strip() == b.split('hex ')[1].strip()
+    vals = dict(eval(a.split('vals ')[1].split('\n')[0]))
+    assert vals == {'a': 10.0, 'b': 64.0, 'c': 4.0}, vals

@@ -289,12 +289,18 @@ def test_value_lattice_bitwise_equals_per_candidate(name):
 def test_fit_suggest_matches_fit_then_suggest(name):
     """tpe_plan_fit_suggest (one engine call) equals fit() + suggest() bit for
     bit on every test space, for single and batched suggestions (up to the 8
-    inline seeds) and candidate counts from n_EI=24 to beyond 8192."""
+    inline seeds) and candidate counts from n_EI=24 to beyond 8192; on
+    config 2 also a sorted draw on one-row wave tiles (2^18 candidates, the
+    config-3 regime), where both paths read the moment table the fit wrote
+    (mom_width: the same table whichever entry point fitted)."""
     meta, d, dom, trials = _fixture_trials(name)
     tpe.suggest([meta['new_id']], dom, trials, 7, n_EI_candidates=64)
     plan = dom._tpe_state.plan
-    for seeds, n in [([3], 24), ([4], 4096), ([5, 6, 7], 2000), ([8], 8192), ([9], 8193),
-                     ([1, 2, 3, 4, 5, 6, 7, 8], 1024)]:
+    shapes = [([3], 24), ([4], 4096), ([5, 6, 7], 2000), ([8], 8192), ([9], 8193),
+              ([1, 2, 3, 4, 5, 6, 7, 8], 1024)]
+    if name == 'cfg2':
+        shapes.append(([10], 1 << 18))
+    for seeds, n in shapes:
         got = plan.fit_suggest(seeds, n)
         plan.fit()
         want = plan.suggest(seeds, n)

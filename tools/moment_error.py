@@ -62,7 +62,7 @@ def mixture(cfg, hp_i):
         x = U[:, hp_i]
         lo, hi = -5.0, 5.0
     else:
-        n = 1000 if cfg == 'cfg5' else 1400
+        n = int(os.environ.get('MOM_N', 1000 if cfg == 'cfg5' else 1400))
         rs = np.random.RandomState(hp_i + 3)
         x = rs.uniform(-5, 5, n)
         L = np.random.RandomState(2).rand(n)
