@@ -1,0 +1,16 @@
+set -euo pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r6_03; mkdir -p $O
+rc=0; timeout -k 10 900 python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu tests/ > $O/tests.log 2>&1 || rc=$?
+# (assertion failures only: anything else ends the job here)
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 300 python -u bench.py --config cfg5 --steps 2 --warmup 1 --no-cpu-baseline --no-e2e > $O/b_cfg5.json 2> $O/b_cfg5.err
+TPE_MOMENT=0 timeout -k 10 300 python -u bench.py --config cfg5 --steps 2 --warmup 1 --no-cpu-baseline --no-e2e > $O/b_cfg5_nomom.json 2> $O/b_cfg5_nomom.err
+timeout -k 10 300 python -u bench.py --config cfg3 --steps 50 --no-cpu-baseline --no-e2e > $O/b_cfg3.json 2> $O/b_cfg3.err
+TPE_MOMENT=0 timeout -k 10 300 python -u bench.py --config cfg3 --steps 50 --no-cpu-baseline --no-e2e > $O/b_cfg3_nomom.json 2> $O/b_cfg3_nomom.err
+timeout -k 10 300 python -u bench.py --steps 5 --no-cpu-baseline --no-e2e > $O/b_cfg4.json 2> $O/b_cfg4.err
+timeout -k 10 300 python -u bench.py --config cfg2 --steps 100 --no-cpu-baseline --no-e2e > $O/b_cfg2.json 2> $O/b_cfg2.err
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/p5 -o p5 -- python3 -u $GRAFT_REPO_ROOT/bench.py --config cfg5 --steps 1 --warmup 1 --no-cpu-baseline --no-e2e > $GRAFT_REPO_ROOT/$O/p5.json 2> $GRAFT_REPO_ROOT/$O/p5.err
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/p4 -o p4 -- python3 -u $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-e2e > $GRAFT_REPO_ROOT/$O/p4.json 2> $GRAFT_REPO_ROOT/$O/p4.err
+echo done

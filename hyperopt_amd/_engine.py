@@ -562,10 +562,13 @@ class Plan(object):
         log-sum-exp evaluated, of those in the fp32 per-group-lift form[,
         one-exponent pairs re-evaluated by a wave's second attempt,
         one-exponent pairs of wide blocks (mode 3's fp64 loop), one-exponent
-        pairs evaluated in the moment form of their chunk]) -- the first ``n``
-        (7, 9 or 10); enable it for the following suggests."""
+        pairs evaluated in the moment form of their chunk, of those the
+        8-wide form]) -- the first ``n`` (7 .. 11); enable it for the
+        following suggests."""
+        if not 0 <= n <= 11:
+            raise ValueError('the census has 11 counters')
         e = self.engine
-        out = (C.c_int64 * 10)()
+        out = (C.c_int64 * 11)()
         with e.lock:
             e.check(e.lib.tpe_plan_census_n(self.p, int(bool(enable)), out, int(n)))
         return tuple(int(v) for v in out[:n])

@@ -193,13 +193,17 @@ __device__ void build_table(const tpe_hp &H, int K, const double *__restrict__ w
 // cancellation in 1 - x, full range of y), both branches evaluated without
 // divergence; beyond w = 36 (y < ~1e-16, outside the fitted range) the fp64
 // OCML erfcinv.
+// (the fp64 OCML erfcinv of the far tail out of line: inlined, its
+// temporaries set the register allocation of every draw loop that can reach
+// it -- k_draw_sorted went from 142 to 255 VGPRs)
+__device__ __attribute__((noinline)) inline double erfcinv_ool(double y) { return erfcinv(y); }
 __device__ __forceinline__ double erfcinv_fast(double y) {
   int e1, e2;
   const double m1 = frexp(y, &e1), m2 = frexp(2.0 - y, &e2);
   const float l2 = __builtin_amdgcn_logf((float)m1) + __builtin_amdgcn_logf((float)m2) +
                    (float)(e1 + e2);                   // log2(y (2 - y))
   const float w = -0.6931471805599453f * l2;
-  if (!(w <= 36.0f)) return erfcinv(y);
+  if (!(w <= 36.0f)) return erfcinv_ool(y);
   const float wc = w - 2.5f;
   float pc = 2.81022636e-08f;
   pc = fmaf(pc, wc, 3.43273939e-07f);
@@ -559,7 +563,11 @@ struct SortedDrawLds {
 // EXT (k_sort_ext): the values come from src[slot][n_cand] instead of the
 // draw (given candidates scored exactly as a large draw's are).  Every
 // thread of the block calls it.
-template <int CAP, int NT, bool EXT>
+// FAST: the launch's drawn slots are all bounded continuous ones with a
+// table (the host checks it, launch_draw_sorted): only the inline draw is
+// compiled in -- no out-of-line draw call, whose calling convention would
+// set the kernel's registers (143 VGPRs against ~60)
+template <int CAP, int NT, bool EXT, bool FAST = false>
 __device__ __forceinline__ void sorted_block_body(const ScoreArgs &A, int slot, int s,
                                                   int64_t base, bool bucket, bool lg,
                                                   int32_t *__restrict__ pos_out,
@@ -594,8 +602,8 @@ __device__ __forceinline__ void sorted_block_body(const ScoreArgs &A, int slot, 
   // bounded continuous slots with a table (config 4 / 5's hps): the table
   // draw inline with the descriptor in scalar registers (draw_bounded_inline,
   // the same values); everything else through the out-of-line draws
-  const bool fast = !EXT && tab && H.family != TPE_CAT && (H.flags & TPE_HAS_LOW) &&
-                    (H.flags & TPE_HAS_HIGH);
+  const bool fast = FAST || (!EXT && tab && H.family != TPE_CAT && (H.flags & TPE_HAS_LOW) &&
+                             (H.flags & TPE_HAS_HIGH));
   if (fast) {
     const double cdf_last = L.T.cdf[K - 1];
     const double high_prev = nextafter(H.high, -INFINITY);
@@ -608,7 +616,7 @@ __device__ __forceinline__ void sorted_block_body(const ScoreArgs &A, int slot, 
       emit(i, draw_bounded_inline<CAP>(L.T, K, cdf_last, bmu, bsg, H.low, H.high, high_prev,
                                        logn, hasq, H.q, r0));
     }
-  } else {
+  } else if constexpr (!FAST) {
 #pragma unroll 1
     for (int i = t; i < n; i += NT) {
       const uint64_t gi = (uint64_t)(A.cand_begin + base + i);

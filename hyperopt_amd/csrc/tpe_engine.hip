@@ -77,6 +77,19 @@ static bool publish_fuse_on() {
   }();
   return on;
 }
+// TPE_L2_WARM=1: scoring tiles first touch every 128-B line of both
+// mixtures' coefficient tables (round 2's L2 warm-up).  Off by default since
+// round 6: the same-box A/B (gpurun_out/r6_05) gave config 4 127.3 -> 124.2 ms
+// and config 5 543 -> 536 ms per step without it -- the waves' first envelope
+// reads waited on those loads, and the tables are L2-resident after the first
+// blocks anyway
+static bool l2_warm_on() {
+  static const bool on = [] {
+    const char *e = std::getenv("TPE_L2_WARM");
+    return e && std::atoi(e) != 0;
+  }();
+  return on;
+}
 static bool side_streams_on() {
   static const bool on = std::getenv("TPE_SIDE_STREAMS") != nullptr;
   return on;
@@ -652,6 +665,7 @@ ScoreArgs base_args(tpe_plan *p, int64_t n_sug) {
   a.lat_info = p->d_lat_info;
   a.lat = p->d_lat;
   a.lse_mom = p->mom_w;
+  a.l2_warm = l2_warm_on() ? 1 : 0;
   return a;
 }
 
@@ -1037,7 +1051,17 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
         pr->n++;
       }
     } else if (sorted_draw) {
-      const hipError_t e = launch_draw_sorted(a, kmax <= kFuseTab, p->d_cpos, st);
+      // the inline-draw kernel when every slot it draws is bounded continuous
+      // (the lookup slots drawn in their tiles are skipped by it); kmax within
+      // the table (table_draw) holds here
+      bool fast = true;
+      for (int i = 0; i < n_level && fast; ++i) {
+        const tpe_hp &x = p->hps[p->levels[level][i]];
+        const bool lookup = ck[i] == KIND_CAT || ck[i] == KIND_LAT;
+        fast = lookup ? (a.lookup_draw != 0 && kmax <= kFuseTab)
+                      : (x.family != TPE_CAT && (x.flags & TPE_HAS_LOW) && (x.flags & TPE_HAS_HIGH));
+      }
+      const hipError_t e = launch_draw_sorted(a, kmax <= kFuseTab, fast, p->d_cpos, st);
       if (e != hipSuccess) { join_lk(); return fail(h, TPE_E_HIP, hipGetErrorString(e)); }
     } else {
       CKH(launch_draw(a, table_draw, st));
@@ -1677,7 +1701,8 @@ namespace {
 int enqueue_step(tpe_engine *h, tpe_plan *p, int32_t nb, double prior_weight, int32_t lf,
                  int64_t n_sug, int64_t n_cand, hipStream_t st) {
   // the moment table only for a step whose suggest takes a sorted draw
-  // (run_level's sorted_draw: n_cand x n_sug x level hps >= 2^22), the only
+  // (run_level's sorted_draw: n_cand x n_sug x level hps >= 2^22) on two-row
+  // wave tiles (> kWaveRowSplitMax candidates per suggestion), the only
   // launches that read it; the others skip its ~3-5 us in k_fit.  Whenever it
   // is read, the table is the one tpe_plan_fit writes (mom_width), so a
   // fit_suggest and a fit + suggest score alike (test_fit_suggest_matches_*)
@@ -1685,7 +1710,8 @@ int enqueue_step(tpe_engine *h, tpe_plan *p, int32_t nb, double prior_weight, in
   for (const auto &l : p->levels)
     sorted |= n_cand * n_sug * (int64_t)l.size() >= ((int64_t)1 << 22);
   {
-    const int rc = fit_launch(h, p, fit_args(p, nb, prior_weight, lf, sorted), p->P, st);
+    const bool mom = sorted && n_cand > kWaveRowSplitMax;
+    const int rc = fit_launch(h, p, fit_args(p, nb, prior_weight, lf, mom), p->P, st);
     if (rc) return rc;
   }
   p->last_nb = nb;

@@ -206,9 +206,10 @@ __host__ __device__ constexpr int64_t mom_stride(int64_t kcap) {
 // one-exponent size up; the scoring kernels are instantiated per width, so the
 // 16-wide kernel's register allocation is the round-5 one.  A block of 8 is
 // one Coef32 block: the same centre (mu' midpoint) and base.  Truncation
-// tau(x) = x^16 / 16! e^x; taken for x <= kMomXLim (tau <= 1e-16) or by the
+// tau(x) = x^16 / 16! e^x; taken for x <= kMom8XLim (tau <= 5.7e-9) or by the
 // weighted criterion as the 16-wide form.  128 B = two 64-B scalar loads.
 constexpr int kMom8Deg = 15;
+constexpr float kMom8XLim = 1.85f;          // tau(1.85) = 5.7e-9, kMomXLim's budget
 constexpr float kMom8Log2Fact = 44.25014f;  // log2(16!)
 constexpr int64_t kMom16MinK = 4000;
 struct __attribute__((aligned(128))) CoefM8 {
@@ -306,6 +307,8 @@ struct ScoreArgs {
                              // lattice) unwritten and the scoring tile draws them itself,
                              // for below mixtures of 1 .. kFuseTab components (lookup_inline)
   int64_t lookup_seg;        // candidates per lookup-scan block (set by the lookup launch)
+  int32_t l2_warm;           // scoring tiles touch their mixtures' coefficient lines first
+                             // (one load per 128-B line; TPE_L2_WARM=1, A/B; default off)
   int32_t tile_draw;         // tiny unsorted draws: every tile draws its own candidates
                              // (k_score_tdraw; no k_draw launch, nothing written)
   const LatInfo *lat_info;   // [P] value lattices (KIND_LAT slots)
@@ -418,7 +421,10 @@ hipError_t launch_draw(const ScoreArgs &a, bool table, hipStream_t st);
 // for the log-sum-exp block skip and the erf dead-zone skip); small_table:
 // every below K <= kFuseTab
 constexpr int kSortedBlock = 4096;
-hipError_t launch_draw_sorted(const ScoreArgs &a, bool small_table, int32_t *pos_out,
+// fast: every slot the launch draws is a bounded continuous one (low and
+// high) whose below mixture fits the table, the rest lookup slots their tiles
+// draw (lookup_draw) -- the kernel without the out-of-line draws
+hipError_t launch_draw_sorted(const ScoreArgs &a, bool small_table, bool fast, int32_t *pos_out,
                               hipStream_t st);
 static_assert(kSortedBlock == TPE_SHARD_ALIGN, "shard alignment is the sorted-draw block");
 // given candidates src[slot][n_cand] (one suggestion) bucketed exactly as

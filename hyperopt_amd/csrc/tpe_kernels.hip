@@ -62,7 +62,7 @@ __device__ __forceinline__ int slot_kind(const ScoreArgs &A, int slot) {
   return -1;
 }
 
-template <int CAP, int NT, bool EXT>
+template <int CAP, int NT, bool EXT, bool FAST = false>
 __device__ __forceinline__ void sorted_block(const ScoreArgs &A, int32_t *__restrict__ pos_out,
                                              const double *__restrict__ src,
                                              SortedDrawLds<CAP, NT> &L) {
@@ -76,16 +76,27 @@ __device__ __forceinline__ void sorted_block(const ScoreArgs &A, int32_t *__rest
   const int kind = slot_kind(A, slot);
   // lookup slots the scoring tile draws itself: nothing to write
   if (!EXT && (kind == KIND_CAT || kind == KIND_LAT) && lookup_inline(A, A.info[2 * hp].K)) return;
-  sorted_block_body<CAP, NT, EXT>(
+  sorted_block_body<CAP, NT, EXT, FAST>(
       A, slot, s, (int64_t)blockIdx.x * kSortedBlock,
       kind_lse(kind) || kind == KIND_ERF_G || kind == KIND_ERF_L, kind_logn(kind), pos_out, src,
       L);
 }
 
 template <int CAP>
-__global__ __launch_bounds__(kDrawThreads) void k_draw_sorted(ScoreArgs A, int32_t *__restrict__ pos_out) {
+// (LDS holds three blocks per CU: three waves per SIMD is the occupancy the
+// registers must allow, <= 168 VGPRs)
+__global__ __launch_bounds__(kDrawThreads) __attribute__((amdgpu_waves_per_eu(CAP <= kFuseTab ? 3 : 1)))
+void k_draw_sorted(ScoreArgs A, int32_t *__restrict__ pos_out) {
   __shared__ SortedDrawLds<CAP, kDrawThreads> L;
   sorted_block<CAP, kDrawThreads, false>(A, pos_out, nullptr, L);
+}
+// levels whose drawn slots are all bounded continuous with a table (configs 4
+// and 5): the inline draw only (sorted_block_body FAST)
+template <int CAP>
+__global__ __launch_bounds__(kDrawThreads) __attribute__((amdgpu_waves_per_eu(CAP <= kFuseTab ? 3 : 1)))
+void k_draw_sorted_fast(ScoreArgs A, int32_t *__restrict__ pos_out) {
+  __shared__ SortedDrawLds<CAP, kDrawThreads> L;
+  sorted_block<CAP, kDrawThreads, false, true>(A, pos_out, nullptr, L);
 }
 
 // The same blocks on 1024 threads, for launches of too few blocks to fill the
@@ -96,6 +107,12 @@ __global__ __launch_bounds__(kWideDrawThreads) void k_draw_sorted_wide(ScoreArgs
                                                                        int32_t *__restrict__ pos_out) {
   __shared__ SortedDrawLds<CAP, kWideDrawThreads> L;
   sorted_block<CAP, kWideDrawThreads, false>(A, pos_out, nullptr, L);
+}
+template <int CAP>
+__global__ __launch_bounds__(kWideDrawThreads) void k_draw_sorted_wide_fast(
+    ScoreArgs A, int32_t *__restrict__ pos_out) {
+  __shared__ SortedDrawLds<CAP, kWideDrawThreads> L;
+  sorted_block<CAP, kWideDrawThreads, false, true>(A, pos_out, nullptr, L);
 }
 
 __global__ __launch_bounds__(kDrawThreads) void k_sort_ext(ScoreArgs A, const double *__restrict__ src,
@@ -647,13 +664,18 @@ hipError_t launch_micro(int which, int blocks, int iters, double *sink, hipStrea
 bool is_draw_kernel_fn(const void *f) {
   return f == reinterpret_cast<const void *>(&k_draw<true>) ||
          f == reinterpret_cast<const void *>(&k_draw<false>) ||
-         f == reinterpret_cast<const void *>(&k_draw_sorted<kFuseTab>) ||
-         f == reinterpret_cast<const void *>(&k_draw_sorted<kTabCap>);
+         is_sorted_draw_kernel_fn(f);
 }
 
 bool is_sorted_draw_kernel_fn(const void *f) {
   return f == reinterpret_cast<const void *>(&k_draw_sorted<kFuseTab>) ||
-         f == reinterpret_cast<const void *>(&k_draw_sorted<kTabCap>);
+         f == reinterpret_cast<const void *>(&k_draw_sorted<kTabCap>) ||
+         f == reinterpret_cast<const void *>(&k_draw_sorted_fast<kFuseTab>) ||
+         f == reinterpret_cast<const void *>(&k_draw_sorted_fast<kTabCap>) ||
+         f == reinterpret_cast<const void *>(&k_draw_sorted_wide<kFuseTab>) ||
+         f == reinterpret_cast<const void *>(&k_draw_sorted_wide<kTabCap>) ||
+         f == reinterpret_cast<const void *>(&k_draw_sorted_wide_fast<kFuseTab>) ||
+         f == reinterpret_cast<const void *>(&k_draw_sorted_wide_fast<kTabCap>);
 }
 
 hipError_t launch_draw(const ScoreArgs &a, bool table, hipStream_t st) {
@@ -668,7 +690,7 @@ hipError_t launch_draw(const ScoreArgs &a, bool table, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_draw_sorted(const ScoreArgs &a, bool small_table, int32_t *pos_out,
+hipError_t launch_draw_sorted(const ScoreArgs &a, bool small_table, bool fast, int32_t *pos_out,
                               hipStream_t st) {
   if (a.n_slots <= 0 || a.n_suggest <= 0 || a.n_cand <= 0) return hipSuccess;
   const unsigned gx = (unsigned)((a.n_cand + kSortedBlock - 1) / kSortedBlock);
@@ -677,8 +699,16 @@ hipError_t launch_draw_sorted(const ScoreArgs &a, bool small_table, int32_t *pos
   // wave per SIMD; the launch is then bound by one block's latency)
   const bool wide = (int64_t)gx * a.slot_rows * a.n_suggest <= 2 * kNumCUs;
   if (wide) {
-    if (small_table) k_draw_sorted_wide<kFuseTab><<<g, kWideDrawThreads, 0, st>>>(a, pos_out);
-    else k_draw_sorted_wide<kTabCap><<<g, kWideDrawThreads, 0, st>>>(a, pos_out);
+    if (fast) {
+      if (small_table) k_draw_sorted_wide_fast<kFuseTab><<<g, kWideDrawThreads, 0, st>>>(a, pos_out);
+      else k_draw_sorted_wide_fast<kTabCap><<<g, kWideDrawThreads, 0, st>>>(a, pos_out);
+    } else {
+      if (small_table) k_draw_sorted_wide<kFuseTab><<<g, kWideDrawThreads, 0, st>>>(a, pos_out);
+      else k_draw_sorted_wide<kTabCap><<<g, kWideDrawThreads, 0, st>>>(a, pos_out);
+    }
+  } else if (fast) {
+    if (small_table) k_draw_sorted_fast<kFuseTab><<<g, kDrawThreads, 0, st>>>(a, pos_out);
+    else k_draw_sorted_fast<kTabCap><<<g, kDrawThreads, 0, st>>>(a, pos_out);
   } else if (small_table) {
     k_draw_sorted<kFuseTab><<<g, kDrawThreads, 0, st>>>(a, pos_out);
   } else {

@@ -254,11 +254,24 @@ __device__ __forceinline__ void mom8_terms2(const Mom8Group &a, const Mom8Group 
 __device__ unsigned g_wave_info[8192][8][4];
 #define WINFO(i, v)                                                                      \
   do {                                                                                   \
-    if ((threadIdx.x & 63) == 0 && blockIdx.y == 0)                                      \
-      g_wave_info[blockIdx.x & 8191][threadIdx.x >> 6][i] += (unsigned)(v);              \
+    if ((threadIdx.x & 63) == 0 && blockIdx.y == 0 && blockIdx.x < 8192)                 \
+      g_wave_info[blockIdx.x][threadIdx.x >> 6][i] += (unsigned)(v);                     \
+  } while (0)
+// per wave (wave tiles), lane 0 of every wave of the blocks of suggestion 0:
+// [0] start of the component loops, [1] their end, [2] after the candidate
+// loads, [3] after the below mixture, [4] after the above mixture's window,
+// [5] after pass 1 of the one-exponent loop, [6] after its tightening, [7]
+// after pass 2 (the guard passed), [8] after the finalize's wave argmax
+constexpr int kWaveStamps = 10;
+__device__ unsigned long long g_wave_stamps[8192][8][kWaveStamps];
+#define WSTAMP(i)                                                                        \
+  do {                                                                                   \
+    if ((threadIdx.x & 63) == 0 && blockIdx.y == 0 && blockIdx.x < 8192)                 \
+      g_wave_stamps[blockIdx.x][threadIdx.x >> 6][i] = wall_clock64();                   \
   } while (0)
 #else
 #define WINFO(i, v) do {} while (0)
+#define WSTAMP(i) do {} while (0)
 #endif
 typedef const float4 __attribute__((address_space(3))) LF4;
 typedef const Coef32 __attribute__((address_space(3))) LC32;
@@ -674,6 +687,7 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
   float wmax = bmax;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) wmax = fmaxf(wmax, __shfl_xor(wmax, o, 64));
+  if (STRIDE == 1) WSTAMP(5);
   if (!(wmax > -INFINITY && wmax < INFINITY)) return false;  // non-finite envelope
   {
     // a tighter skip threshold: every lane's largest term is at least its
@@ -735,6 +749,7 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
     }
   }
   bmax = wmax;
+  if (STRIDE == 1) WSTAMP(6);
   // pass 2 with M = ceil(bmax) + 1 for every lane; a lane whose sum comes
   // out below 2^-4 re-centres on its own sum (M + ceil(log2 s) + 1, the sum
   // then in (1/4, 1/2]) and the wave runs once more; failing that (or a sum
@@ -819,7 +834,7 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
             const float x = fmaxf(fabsf(win.lo - cf), fabsf(win.hi - cf)) * q->xh;
             const float l2tau = (float)(kMom8Deg + 1) * __builtin_amdgcn_logf(x) +
                                 x * 1.44269504f - kMom8Log2Fact;
-            elig = x <= kMomXLim || (x <= kMomXCap && l2tau + bnd <= win.thr + 1.0f);
+            elig = x <= kMom8XLim || (x <= kMomXCap && l2tau + bnd <= win.thr + 1.0f);
           }
           cmask = __ballot(live && elig);
         } else {
@@ -1070,7 +1085,58 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
   }
 #pragma unroll
   for (int r = 0; r < KR; ++r) out[r] = (y[r] != y[r]) ? LseAcc{NAN, NAN} : LseAcc{M, s[r]};
+  if (STRIDE == 1) WSTAMP(7);
   return true;
+}
+
+// Mixtures of at most kSmallMix components on wave tiles (the good side: K_b
+// = n_below + 1 <= 26) -- an exact two-pass log-sum-exp straight from the
+// block's LDS copy of the coefficients: the lane's largest term m (the same
+// fp64 t = alpha + y'(beta + gamma y') as lse_terms), then the terms 2^(t -
+// ceil m) summed in fp32 over runs of 8 and in fp64 across them.  No envelope
+// round, window, scalar coefficient loads or per-group lift: the envelope /
+// fp64 lift loop these mixtures took (their blocks are wide in sigma units,
+// so never in the fp32 form) spent ~7 us per config-5 wave waiting on loads.
+// Output as lse_chunks': NaN for a NaN candidate, (-inf, 0) when every term
+// is -inf, a NaN term makes the sum NaN.
+constexpr int kSmallMix = 32;
+template <int KR>
+__device__ __forceinline__ void lse_small(const double (*__restrict__ cf)[kSmallMix], int K,
+                                          const double (&y)[KR], LseAcc (&out)[KR]) {
+  double y2[KR], m[KR];
+#pragma unroll
+  for (int r = 0; r < KR; ++r) { y2[r] = y[r] * y[r]; m[r] = -INFINITY; }
+  for (int k = 0; k < K; ++k) {
+    const double cx = cf[0][k], cy = cf[1][k], cz = cf[2][k];
+#pragma unroll
+    for (int r = 0; r < KR; ++r) m[r] = fmax(m[r], fma(cz, y2[r], fma(cy, y[r], cx)));
+  }
+  double ms[KR], sd[KR];
+  float sf[KR];
+#pragma unroll
+  for (int r = 0; r < KR; ++r) {
+    m[r] = ceil(m[r]);
+    ms[r] = m[r] == -INFINITY ? 0.0 : m[r];
+    sd[r] = 0.0;
+    sf[r] = 0.0f;
+  }
+  for (int k = 0; k < K; ++k) {
+    const double cx = cf[0][k], cy = cf[1][k], cz = cf[2][k];
+#pragma unroll
+    for (int r = 0; r < KR; ++r)
+      sf[r] += __builtin_amdgcn_exp2f((float)(fma(cz, y2[r], fma(cy, y[r], cx)) - ms[r]));
+    if ((k & 7) == 7) {
+#pragma unroll
+      for (int r = 0; r < KR; ++r) { sd[r] += (double)sf[r]; sf[r] = 0.0f; }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < KR; ++r) {
+    sd[r] += (double)sf[r];
+    if (y[r] != y[r]) out[r] = LseAcc{NAN, NAN};
+    else if (m[r] == -INFINITY) out[r] = sd[r] == 0.0 ? LseAcc{-INFINITY, 0.0} : LseAcc{NAN, NAN};
+    else out[r] = LseAcc{m[r], sd[r]};
+  }
 }
 
 // PRUNE setup, part 1 (once per wave, shared by both mixtures): the wave's
@@ -1276,8 +1342,8 @@ __device__ unsigned long long g_score_stamps[8192][4];
 #endif
 #define SSTAMP(i)                                                                        \
   do {                                                                                   \
-    if (STAMP_KIND_OK && threadIdx.x == 0 && blockIdx.y == 0) {                          \
-      const unsigned b = blockIdx.x & 8191;                                              \
+    if (STAMP_KIND_OK && threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.x < 8192) {     \
+      const unsigned b = blockIdx.x;                                                     \
       g_score_stamps[b][i] = wall_clock64();                                             \
       if (i == 0)                                                                        \
         g_score_stamps[b][3] =                                                           \
@@ -1287,18 +1353,8 @@ __device__ unsigned long long g_score_stamps[8192][4];
             (__builtin_amdgcn_s_getreg(63488 | 4) & 0xffff);                             \
     }                                                                                    \
   } while (0)
-// per wave (wave tiles): start and end of the component loops ([0], [1]),
-// after the candidate loads ([2]) and after the below mixture ([3]), lane 0 of
-// every wave of the blocks of suggestion 0
-__device__ unsigned long long g_wave_stamps[8192][kWaves][4];
-#define WSTAMP(i)                                                                        \
-  do {                                                                                   \
-    if ((threadIdx.x & 63) == 0 && blockIdx.y == 0)                                      \
-      g_wave_stamps[blockIdx.x & 8191][threadIdx.x >> 6][i] = wall_clock64();            \
-  } while (0)
 #else
 #define SSTAMP(i) do {} while (0)
-#define WSTAMP(i) do {} while (0)
 #endif
 
 template <int R>
@@ -1311,6 +1367,8 @@ struct ScoreSmemT {
   int64_t best_li[kWaves];
 #endif
   uint32_t arrive;                      // wave tiles: waves done with the tile
+  double small[2][3][kSmallMix];        // wave tiles: mixtures of <= kSmallMix components
+                                        //   (alpha, beta, gamma rows; below, above), lse_small
   DrawTableT<kFuseTab> dt;              // lookup tiles drawing their candidates (lookup_inline)
   double top_s;                         // lookup scans: the best score any value can get
   int top_nan;                          //   (a NaN score: top is NaN)
@@ -1422,6 +1480,20 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
   bool staged = false;
   if constexpr (WT) {  // the block's arrival counter (finalize), before any wave can arrive
     if (threadIdx.x == 0) sm.arrive = 0u;
+    // small mixtures' coefficients (lse_small) into LDS: thread t of the first
+    // 2 x kSmallMix copies component t % kSmallMix of mixture t / kSmallMix
+    if constexpr (LSE) {
+      if (threadIdx.x < 2 * kSmallMix) {
+        const int q = threadIdx.x / kSmallMix, k = threadIdx.x % kSmallMix;
+        const int Kq = q ? ia.K : ib.K;
+        if (Kq <= kSmallMix && k < Kq && A.lse_prune != 0) {
+          const double *t = reinterpret_cast<const double *>(A.coef + (q ? sa : sb) * A.kcap);
+          sm.small[q][0][k] = t[coef_off(k, 0)];
+          sm.small[q][1][k] = t[coef_off(k, 1)];
+          sm.small[q][2][k] = t[coef_off(k, 2)];
+        }
+      }
+    }
     if constexpr (STAGE) {
       staged = nbb + nba <= kStageBlocks && A.lse_prune > 2;  // block-uniform
       if (staged) {
@@ -1568,7 +1640,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
     // 128-B line, issued before the component loop, so the loop's scalar loads
     // hit L2 instead of each group paying a far (MALL / HBM) round trip
     float sink = 0.f;
-    {
+    if (A.l2_warm) {
       const int nlb = (ib.K + 3) >> 2, nla = (ia.K + 3) >> 2;
       for (int i = threadIdx.x; i < nlb + nla; i += blockDim.x) {
         const Coef *c = i < nlb ? cb + 4 * i : ca + 4 * (i - nlb);
@@ -1633,8 +1705,22 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
           }
           continue;
         }
+        if (WT && prune && K <= kSmallMix) {
+          // a small mixture (the good side): the direct exact two-pass sum
+          lse_small<KR>(sm.small[mix], K, y, lacc[mix]);
+          if constexpr (CENSUS) {
+            lcen.total += (uint32_t)(K * nvalid);
+            lcen.exec += (uint32_t)(K * nvalid);
+          }
+#pragma unroll
+          for (int r = 0; r < KR; ++r)
+            sm.wpart[mix][wave][r][lane] = make_double2(lacc[mix][r].m, lacc[mix][r].s);
+          if (mix == 0) WSTAMP(3);
+          continue;
+        }
         LseWindow win{0.0f, 0.0f, -INFINITY};
         if (prune) win = lse_window<KR>(uniform_ptr(cm), mix ? ia.probe : ib.probe, K, y, valid, rg);
+        if (WT && mix == 1) WSTAMP(4);
         // shifted single-exponent loop when the wave's window allows it
         // (lse_chunks_shifted's guard), else the exact per-group-lift loop
         // (mixtures of >= lse_shift_min components: fewer leave too few
@@ -1653,10 +1739,16 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
         if (prune && A.lse_prune > 1 && K >= A.lse_shift_min && win.thr > -INFINITY) {
           // (the moment table of the launch's width: CoefM chunks or CoefM8 blocks)
           const int64_t ms = mix ? sa : sb;
-          const CoefM *mt16 =
-              (MW == 16 && A.lse_mom == 16) ? A.coefm + ms * mom_stride(A.kcap) : nullptr;
-          const CoefM8 *mt8 =
-              (MW == 8 && A.lse_mom == 8) ? A.coefm8 + ms * (A.kcap / kCoefBlock) : nullptr;
+          // (two-row wave tiles only: the one-row tiles of <= 2^18 candidates
+          // -- config 3 -- are bound by per-wave latency, 0.5 live blocks per
+          // wave, and the form's eligibility loads only add to it: 33 -> 71 us
+          // per config-3 level-2 launch with it.  Never reading it there also
+          // keeps fit_suggest, which writes the table only for two-row
+          // steps, equal to fit + suggest)
+          const CoefM *mt16 = (KR == 2 && MW == 16 && A.lse_mom == 16)
+                                  ? A.coefm + ms * mom_stride(A.kcap) : nullptr;
+          const CoefM8 *mt8 = (KR == 2 && MW == 8 && A.lse_mom == 8)
+                                  ? A.coefm8 + ms * (A.kcap / kCoefBlock) : nullptr;
           if (STAGE && staged)  // (prune mode 3 only: the staged blocks are Coef32)
             shifted = lse_chunks_shifted<KR, CENSUS, ST, true, STAGE, MW>(
                 uniform_ptr(cm), cm, cw0, K, y, valid, lacc[mix], win, nvalid, lcen,
@@ -1924,6 +2016,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
 #else
   wave_best(best_s, best_v, best_i);
 #endif
+  if constexpr (WT) WSTAMP(8);
   if constexpr (WT) {
     // the block's argmax over its wave tiles without a block barrier: each
     // wave leaves its record in LDS and arrives on the block's LDS counter;

@@ -67,9 +67,10 @@ def main(cfg, n_cand):
               (sl, (slot == sl).sum(), r[:, 0].min(), r[:, 0].max(), (r[:, 1] - r[:, 0]).mean(),
                (r[:, 1] - r[:, 0]).max(), (r[:, 2] - r[:, 1]).mean(), r[:, 2].max()))
     # per wave (wave tiles): component-loop durations and the block ends
-    wb = (C.c_ulonglong * (8192 * 8 * 4))()
+    NS = 10  # tpe_score.hip kWaveStamps
+    wb = (C.c_ulonglong * (8192 * 8 * NS))()
     if hasattr(eng.lib, 'tpe_debug_wave_stamps') and eng.lib.tpe_debug_wave_stamps(wb) == 0:
-        ws = np.frombuffer(wb, dtype=np.uint64).reshape(8192, 8, 4).astype(np.int64)[:nb]
+        ws = np.frombuffer(wb, dtype=np.uint64).reshape(8192, 8, NS).astype(np.int64)[:nb]
         okw = (ws[:, :, 0] > 0) & (ws[:, :, 1] >= ws[:, :, 0])
         if okw.any():
             t0 = t[:, 0].min()
@@ -102,7 +103,7 @@ def main(cfg, n_cand):
                   (bend[sel].mean(), bend[sel].max(), bend[sel].max() / bend[sel].mean()))
             # loop time by the wave's place in its 4096-candidate sort block
             # (dense value windows), from the tile mapping of tpe_score.hip
-            if (ws[:, :, 2:] > 0).all(axis=2)[okw].any():
+            if (ws[:, :, 2:4] > 0).all(axis=2)[okw].any():
                 ok4 = okw & (ws[:, :, 2] > 0) & (ws[:, :, 3] > 0)
                 ph = [(ws[:, :, 2] - ws[:, :, 0]), (ws[:, :, 3] - ws[:, :, 2]),
                       (ws[:, :, 1] - ws[:, :, 3])]
@@ -110,6 +111,18 @@ def main(cfg, n_cand):
                     a = a[ok4] / 100.0
                     print('  %-14s mean %6.2f us  p50 %6.2f  p90 %6.2f  max %6.2f' %
                           (nm, a.mean(), np.median(a), np.quantile(a, 0.9), a.max()))
+                # the above mixture's one-exponent loop by phase (waves that
+                # stamped every point: the shifted loop ran and passed)
+                okf = ok4 & (ws[:, :, 4:9] > 0).all(axis=2)
+                if okf.any():
+                    seq = [(3, 4, 'above: window'), (4, 5, 'above: pass 1'),
+                           (5, 6, 'above: tightening'), (6, 7, 'above: pass 2 + guard'),
+                           (7, 1, 'above: to loop end'), (1, 8, 'finalize (wave argmax)')]
+                    print('  above-mixture phases over %d waves (us):' % okf.sum())
+                    for a0, a1, nm in seq:
+                        a = (ws[:, :, a1] - ws[:, :, a0])[okf] / 100.0
+                        print('    %-24s mean %6.2f  p50 %6.2f  p90 %6.2f  max %6.2f' %
+                              (nm, a.mean(), np.median(a), np.quantile(a, 0.9), a.max()))
             if hasattr(eng.lib, 'tpe_debug_wave_info') and lv >= 0:
                 ib = (C.c_uint * (8192 * 8 * 4))()
                 assert eng.lib.tpe_debug_wave_info(ib) == 0
