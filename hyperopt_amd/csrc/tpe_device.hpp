@@ -212,7 +212,8 @@ __device__ __forceinline__ Coef make_coef(const tpe_hp &H, double w, double mu, 
 // as 4 floats rounded outward (tpe_internal.hpp, kLseDeadBase).  NaN terms
 // disable the skip of the block.
 __device__ __forceinline__ void store_lse_envelope(Coef *table, int64_t k, EnvTerm e, bool valid,
-                                                   const Coef &cf, Coef32 *t32) {
+                                                   const Coef &cf, Coef32 *t32,
+                                                   float4 *te = nullptr) {
   // padding lanes (valid = false) contribute the neutral element
   double lo = valid ? e.m : INFINITY, hi = valid ? e.m : -INFINITY;
   double cm = !valid ? -INFINITY : (e.c == e.c) ? e.c : INFINITY, am = valid ? e.a2 : INFINITY;
@@ -267,6 +268,7 @@ __device__ __forceinline__ void store_lse_envelope(Coef *table, int64_t k, EnvTe
   out[3] = ((double)fa > am) ? nextafterf(fa, 0.0f) : fa;
   if (bad) { out[2] = INFINITY; out[3] = 0.0f; }
   if (wide) out[3] = -out[3];  // the block keeps the fp64 quadratic in mode 3
+  if (te) te[k / kCoefBlock] = make_float4(out[0], out[1], out[2], out[3]);  // (compact copy)
 }
 
 // reductions over the 16 lanes of a DPP row (every lane of the row active;

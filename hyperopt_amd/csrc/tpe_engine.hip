@@ -133,6 +133,7 @@ struct tpe_plan {
   Coef32 *d_coef32 = nullptr;  // [2P][kcap / kCoefBlock] block-local fp32 LSE terms
   CoefM *d_coefm = nullptr;    // [2P][mom_stride(kcap)] moment form of 16-component chunks
   CoefM8 *d_coefm8 = nullptr;  // [2P][kcap / kCoefBlock] moment form of 8-component blocks
+  float4 *d_coefe = nullptr;   // [2P][kcap / kCoefBlock] compact log-sum-exp block envelopes
   std::vector<double> act_frac;  // per hp: expected share of the trials it is active in
   int64_t n = 0;  // history length
   // suggestion state
@@ -263,7 +264,7 @@ void plan_free_buffers(tpe_plan *p) {
                   p->d_msig, p->d_scratch, p->d_info, p->d_coef, p->d_results, p->d_seeds,
                   p->d_partial, p->d_ext, p->d_lb, p->d_la, p->d_cand, p->d_cpos,
                   p->d_ticket, p->d_sortbuf, p->d_census, p->d_lat_info, p->d_lat, p->d_coef32, p->d_coefm,
-                  p->d_coefm8};
+                  p->d_coefm8, p->d_coefe};
   for (void *b : bufs) dfree(b);
   if (p->h_results) (void)hipHostFree(p->h_results);
   p->h_results = nullptr;
@@ -445,6 +446,7 @@ int plan_build(tpe_engine *h, const tpe_space *sp, int64_t max_trials, tpe_plan 
   CKH(dalloc(&p->d_coef32, (size_t)slots * (kcap / kCoefBlock)));
   CKH(dalloc(&p->d_coefm, (size_t)slots * mom_stride(kcap)));
   CKH(dalloc(&p->d_coefm8, (size_t)slots * (kcap / kCoefBlock)));
+  CKH(dalloc(&p->d_coefe, (size_t)slots * (kcap / kCoefBlock)));
   // expected activity of every hp (mom_width): an hp conditioned on branch b
   // of a categorical parent is active in ~1 / upper of the parent's trials
   // (levels are in dependency order: parents first)
@@ -651,6 +653,7 @@ ScoreArgs base_args(tpe_plan *p, int64_t n_sug) {
   a.coef32 = p->d_coef32;
   a.coefm = p->d_coefm;
   a.coefm8 = p->d_coefm8;
+  a.coefe = p->d_coefe;
   a.mw = p->d_mw;
   a.mmu = p->d_mmu;
   a.msig = p->d_msig;
@@ -713,6 +716,7 @@ FitArgs fit_args(tpe_plan *p, int32_t n_below, double prior_weight, int32_t lf, 
   a.coef32 = p->d_coef32;
   a.coefm = p->mom_w == 16 ? p->d_coefm : nullptr;
   a.coefm8 = p->mom_w == 8 ? p->d_coefm8 : nullptr;
+  a.coefe = p->d_coefe;
   a.kcap = p->kcap;
   a.ob = p->d_scratch;
   a.tmp = p->d_scratch;
@@ -1436,7 +1440,7 @@ int tpe_score(tpe_handle_t h, int32_t family, const double *x, int64_t n, const 
   rc = put_mixture(h, p, 1, wa, ma, sa, ka, kind);
   if (rc) return rc;
   CKH(launch_prep(p->d_hps, 1, p->d_mw, p->d_mmu, p->d_msig, p->d_info, p->d_coef, p->d_coef32,
-                  p->d_coefm, nullptr, p->kcap, p->d_scratch, h->stream));
+                  p->d_coefm, nullptr, p->d_coefe, p->kcap, p->d_scratch, h->stream));
   p->mom_w = moment_on() ? 16 : 0;
   rc = ensure_ext(h, p, n);
   if (rc) return rc;
@@ -1485,7 +1489,7 @@ int tpe_sample(tpe_handle_t h, int32_t family, const double *w, const double *mu
   rc = put_mixture(h, p, 1, w, mu, sigma, k, kind);
   if (rc) return rc;
   CKH(launch_prep(p->d_hps, 1, p->d_mw, p->d_mmu, p->d_msig, p->d_info, p->d_coef, p->d_coef32,
-                  p->d_coefm, nullptr, p->kcap, p->d_scratch, h->stream));
+                  p->d_coefm, nullptr, p->d_coefe, p->kcap, p->d_scratch, h->stream));
   p->mom_w = moment_on() ? 16 : 0;
   rc = ensure_ext(h, p, n);
   if (rc) return rc;

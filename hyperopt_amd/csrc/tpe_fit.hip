@@ -101,6 +101,7 @@ struct FitShared {
   uint64_t vand[kFitWaves], vor[kFitWaves];
   int wsum[kFitWaves + 1];
   int isum[kFitWaves];
+  float envc[kFitWaves], enva[kFitWaves];  // envelope extremes (envelope_extremes)
   int m, nlt;
 };
 
@@ -809,8 +810,9 @@ __device__ __forceinline__ Split compute_split(const FitArgs &A, const FitCtx &C
 // padding components of the last block (alpha = -inf: terms exactly 0).
 // ------------------------------------------------------------------------
 __device__ __forceinline__ void store_table(const tpe_hp &H, Coef *cf, Coef32 *cf32, CoefM *cfm,
-                                            CoefM8 *cfm8, int K, const double *w, const double *mu,
-                                            const double *sg, double pacc, bool quant) {
+                                            CoefM8 *cfm8, float4 *cfe, int K, const double *w,
+                                            const double *mu, const double *sg, double pacc,
+                                            bool quant) {
   const int kp = (K + kCoefBlock - 1) / kCoefBlock * kCoefBlock;
   const int kp16 = (K + kMomChunk - 1) / kMomChunk * kMomChunk;
   // kp and the block size are multiples of 8: the 8 lanes of a block's
@@ -825,11 +827,45 @@ __device__ __forceinline__ void store_table(const tpe_hp &H, Coef *cf, Coef32 *c
                         : Coef{-INFINITY, 0.0, 0.0, 0.0};
     if (k < kp) {
       store_coef(cf, k, c, quant);
-      if (!quant) store_lse_envelope(cf, k, e, real, c, cf32);
+      if (!quant) store_lse_envelope(cf, k, e, real, c, cf32, cfe);
       if (!quant && cfm8) store_lse_moments8(cfm8, k, e, real);
     }
     if (!quant && cfm) store_lse_moments(cfm, k, e, real);
   }
+}
+
+// The extremes of a log-sum-exp table's block envelopes outside the probe's
+// block (MixInfo::env_cmax / env_amin, for the scoring waves' live-range
+// search): max c (e.z) and min a^2 (|e.w|, the sign flags a wide block), as
+// stored.  Block-wide (after the table's stores: one barrier first); every
+// thread returns them.
+__device__ __forceinline__ float2 envelope_extremes(const Coef *cf, int K, int probe,
+                                                    FitShared &sm) {
+  __syncthreads();
+  const int nb = (K + kCoefBlock - 1) / kCoefBlock, pb = probe >= 0 ? probe / kCoefBlock : -1;
+  const double *t = reinterpret_cast<const double *>(cf);
+  float cmax = -INFINITY, amin = INFINITY;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+    if (b == pb) continue;
+    const float *e = reinterpret_cast<const float *>(t + coef_off((int64_t)b * kCoefBlock, 3));
+    cmax = fmaxf(cmax, e[2] == e[2] ? e[2] : INFINITY);
+    amin = fminf(amin, fabsf(e[3]));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    cmax = fmaxf(cmax, __shfl_xor(cmax, o, 64));
+    amin = fminf(amin, __shfl_xor(amin, o, 64));
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) { sm.envc[wv] = cmax; sm.enva[wv] = amin; }
+  __syncthreads();
+  cmax = -INFINITY;
+  amin = INFINITY;
+  for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+    cmax = fmaxf(cmax, sm.envc[w]);
+    amin = fminf(amin, sm.enva[w]);
+  }
+  return make_float2(cmax, amin);
 }
 
 // ------------------------------------------------------------------------
@@ -840,13 +876,14 @@ __device__ __forceinline__ void store_table(const tpe_hp &H, Coef *cf, Coef32 *c
 // would put that copy on the scratch stack when the call is not inlined)
 __device__ __forceinline__ void prep_slot(const tpe_hp *Hg, int64_t slot, int K, const double *w, const double *mu,
                           const double *sg, MixInfo *info, Coef *coef, Coef32 *coef32,
-                          CoefM *coefm, CoefM8 *coefm8, int64_t kcap, double *tmp,
-                          FitShared &sm) {
+                          CoefM *coefm, CoefM8 *coefm8, float4 *coefe, int64_t kcap,
+                          double *tmp, FitShared &sm) {
   const tpe_hp H = *Hg;
   Coef *cf = coef + slot * kcap;
   Coef32 *cf32 = coef32 + slot * (kcap / kCoefBlock);
   CoefM *cfm = coefm ? coefm + slot * mom_stride(kcap) : nullptr;
   CoefM8 *cfm8 = coefm8 ? coefm8 + slot * (kcap / kCoefBlock) : nullptr;
+  float4 *cfe = coefe ? coefe + slot * (kcap / kCoefBlock) : nullptr;
   const double wsum = block_np_sum(w, K, sm);
   STAMP(7);
   if (H.family == TPE_CAT) {
@@ -858,7 +895,7 @@ __device__ __forceinline__ void prep_slot(const tpe_hp *Hg, int64_t slot, int K,
     if (threadIdx.x == 0) {
       MixInfo mi;
       mi.K = K; mi.kind = 2; mi.p_accept = 1.0; mi.log_pacc = 0.0; mi.wsum = wsum;
-      mi.probe = -1; mi.pad = 0;
+      mi.probe = -1; mi.env_cmax = 0.0f; mi.env_amin = 0.0f; mi.pad2 = 0;
       info[slot] = mi;
     }
     return;
@@ -873,11 +910,11 @@ __device__ __forceinline__ void prep_slot(const tpe_hp *Hg, int64_t slot, int K,
   }
   STAMP(8);
   const bool quant = (H.flags & TPE_HAS_Q) != 0;
-  store_table(H, cf, cf32, cfm, cfm8, K, w, mu, sg, pacc, quant);
+  store_table(H, cf, cf32, cfm, cfm8, cfe, K, w, mu, sg, pacc, quant);
   if (threadIdx.x == 0) {
     MixInfo mi;
     mi.K = K; mi.kind = quant ? 1 : 0; mi.p_accept = pacc; mi.log_pacc = log(pacc);
-    mi.wsum = wsum; mi.probe = -1; mi.pad = 0;
+    mi.wsum = wsum; mi.probe = -1; mi.env_cmax = 0.0f; mi.env_amin = 0.0f; mi.pad2 = 0;
     info[slot] = mi;
   }
 }
@@ -976,15 +1013,21 @@ __device__ __forceinline__ void fit_continuous(const FitArgs &A, const FitCtx &C
   Coef32 *cf32 = A.coef32 + slot * (A.kcap / kCoefBlock);
   CoefM *cfm = A.coefm ? A.coefm + slot * mom_stride(A.kcap) : nullptr;
   CoefM8 *cfm8 = A.coefm8 ? A.coefm8 + slot * (A.kcap / kCoefBlock) : nullptr;
+  float4 *cfe = A.coefe ? A.coefe + slot * (A.kcap / kCoefBlock) : nullptr;
   if (MIXLDS)
     for (int k = threadIdx.x; k < K; k += blockDim.x) { gw[k] = w[k]; gm[k] = mu[k]; gs[k] = sg[k]; }
-  store_table(H, cf, cf32, cfm, cfm8, K, w, mu, sg, pacc, quant);
+  store_table(H, cf, cf32, cfm, cfm8, cfe, K, w, mu, sg, pacc, quant);
+  // (block-uniform: K, quant)
+  const float2 ex = (!quant && K >= kRangeMinK) ? envelope_extremes(cf, K, pos, sm)
+                                                : make_float2(0.0f, 0.0f);
   if (threadIdx.x == 0) {
     MixInfo mi;
     mi.K = K; mi.kind = quant ? 1 : 0; mi.p_accept = pacc; mi.log_pacc = log(pacc);
     mi.wsum = wsum;
     mi.probe = pos;  // the prior: sigma = prior_sigma, the widest after the clip
-    mi.pad = 0;
+    mi.env_cmax = ex.x;
+    mi.env_amin = ex.y > 0.0f && ex.y < INFINITY && ex.x < INFINITY ? ex.y : 0.0f;
+    mi.pad2 = 0;
     A.info[slot] = mi;
   }
 }
@@ -1134,7 +1177,7 @@ __device__ __forceinline__ void categorical_tail(const FitArgs &A, FitShared &sm
   }
   __syncthreads();
   prep_slot(A.hps + slot / 2, slot, upper, w, mu, sg, A.info, A.coef, A.coef32, A.coefm, A.coefm8,
-            A.kcap, A.tmp + slot * A.kcap, sm);
+            A.coefe, A.kcap, A.tmp + slot * A.kcap, sm);
 }
 
 // ------------------------------------------------------------------------
@@ -1385,7 +1428,8 @@ __global__ __launch_bounds__(256) void k_prep(const tpe_hp *__restrict__ hps,
                                               MixInfo *__restrict__ info, Coef *__restrict__ coef,
                                               Coef32 *__restrict__ coef32,
                                               CoefM *__restrict__ coefm,
-                                              CoefM8 *__restrict__ coefm8, int64_t kcap,
+                                              CoefM8 *__restrict__ coefm8,
+                                              float4 *__restrict__ coefe, int64_t kcap,
                                               double *__restrict__ scratch) {
   __shared__ FitShared sm;
   const int hp = blockIdx.x, side = blockIdx.y;
@@ -1393,7 +1437,7 @@ __global__ __launch_bounds__(256) void k_prep(const tpe_hp *__restrict__ hps,
   const int K = info[slot].K;
   __syncthreads();
   prep_slot(hps + hp, slot, K, mw + slot * kcap, mmu + slot * kcap, msig + slot * kcap, info, coef,
-            coef32, coefm, coefm8, kcap, scratch + slot * kcap, sm);
+            coef32, coefm, coefm8, coefe, kcap, scratch + slot * kcap, sm);
 }
 
 // ------------------------------------------------------------------------
@@ -1429,11 +1473,11 @@ hipError_t launch_split(const FitArgs &a, uint8_t *below, hipStream_t st) {
 
 hipError_t launch_prep(const tpe_hp *hps, int32_t n_hp, const double *mw, const double *mmu,
                        const double *msig, MixInfo *info, Coef *coef, Coef32 *coef32,
-                       CoefM *coefm, CoefM8 *coefm8, int64_t kcap, double *scratch,
-                       hipStream_t st) {
+                       CoefM *coefm, CoefM8 *coefm8, float4 *coefe, int64_t kcap,
+                       double *scratch, hipStream_t st) {
   if (n_hp <= 0) return hipSuccess;
   k_prep<<<dim3(n_hp, 2), 256, 0, st>>>(hps, mw, mmu, msig, info, coef, coef32, coefm, coefm8,
-                                        kcap, scratch);
+                                        coefe, kcap, scratch);
   return hipGetLastError();
 }
 

@@ -85,8 +85,16 @@ struct MixInfo {
   double wsum;      // sum of weights (sampler CDF total)
   int32_t probe;    // LSE: a widest component (the Parzen prior), whose term
                     // lower-bounds every candidate's log-sum-exp maximum; -1: none
-  int32_t pad;
+  // LSE tables of >= kRangeMinK components: the largest c (e.z) and the
+  // smallest a^2 (|e.w|) of the block envelopes outside the probe's block, as
+  // stored (rounded outward); env_amin = 0: not computed.  A wave tile's live
+  // blocks other than the probe's then lie within sqrt((cmax - thr) / amin)
+  // of its candidate window (lse_chunks_shifted's range search)
+  float env_cmax;
+  float env_amin;
+  int32_t pad2;
 };
+constexpr int kRangeMinK = 2048;
 
 // Log-sum-exp block envelope (LSE kinds): in the spare w-row of every
 // coefficient block, 4 floats bounding the block's terms
@@ -261,6 +269,7 @@ struct ScoreArgs {
   const Coef32 *coef32;      // [2*P][kcap / kCoefBlock] block-local fp32 LSE terms
   const CoefM *coefm;        // [2*P][mom_stride] moment form of 16-component chunks
   const CoefM8 *coefm8;      // [2*P][kcap / kCoefBlock] moment form of 8-component blocks
+  const float4 *coefe;       // [2*P][kcap / kCoefBlock] log-sum-exp block envelopes, compact
   const double *mw, *mmu, *msig;  // [2*P][kcap] (sampler reads side 0)
   const uint64_t *seeds;     // [S]
   const double *cand;        // candidates [S][n_slots][n_cand] (drawn or external)
@@ -344,6 +353,7 @@ struct FitArgs {
   Coef32 *coef32;            // [2P][kcap / kCoefBlock]
   CoefM *coefm;              // [2P][mom_stride(kcap)] (null: not written)
   CoefM8 *coefm8;            // [2P][kcap / kCoefBlock] (null: not written; at most one of the two)
+  float4 *coefe;             // [2P][kcap / kCoefBlock] compact envelopes (store_lse_envelope)
   int64_t kcap;
   double *ob;                // [2P][kcap] scratch: observations of the slot
   double *tmp;               // [2P][kcap] scratch (may alias ob)
@@ -365,8 +375,8 @@ bool is_sorted_draw_kernel_fn(const void *f);
 const void *lattice_draw_kernel_fn();      // k_lattice<true> (lattice + fused draw)
 hipError_t launch_prep(const tpe_hp *hps, int32_t n_hp, const double *mw,
                        const double *mmu, const double *msig, MixInfo *info,
-                       Coef *coef, Coef32 *coef32, CoefM *coefm, CoefM8 *coefm8, int64_t kcap,
-                       double *scratch, hipStream_t st);
+                       Coef *coef, Coef32 *coef32, CoefM *coefm, CoefM8 *coefm8,
+                       float4 *coefe, int64_t kcap, double *scratch, hipStream_t st);
 // a level mixing wave-tile log-sum-exp groups with other kinds runs two
 // launches: the other kinds on `side` between fork / join events (when side
 // is given; st waits for the join), the log-sum-exp groups on st

@@ -278,6 +278,7 @@ typedef const Coef32 __attribute__((address_space(3))) LC32;
 struct Stage {
   LF4 *env;    // [blocks] envelopes (the Coef w-rows' first 16 B)
   LC32 *c32;   // [blocks] block-local fp32 blocks
+  const float4 *genv;  // the slot's compact envelope table (CoefEnv, global; null: w-rows)
 };
 constexpr int kStageBlocks = 224;  // blocks of both mixtures a workgroup stages (32 KB)
 struct StageSmem {
@@ -296,6 +297,9 @@ __device__ __forceinline__ void load_block32_lds(LC32 *__restrict__ rb, uint32_t
   }
 }
 // the envelope of the block starting at component k0 (global table or stage)
+// (unstaged: the compact envelope table when given -- a round's 64 envelopes
+// are 1 KB contiguous, 8 cache lines, against 64 lines of the Coef w-rows at
+// a 256-B stride)
 template <bool STG>
 __device__ __forceinline__ float4 block_env(const double *tb, const Stage &st, int k0) {
   if constexpr (STG) {
@@ -303,6 +307,7 @@ __device__ __forceinline__ float4 block_env(const double *tb, const Stage &st, i
         (const float __attribute__((address_space(3))) *)(st.env + (k0 >> 3));
     return make_float4(e[0], e[1], e[2], e[3]);
   }
+  else if (st.genv) return st.genv[k0 >> 3];
   else return *reinterpret_cast<const float4 *>(tb + coef_off(k0, 3));
 }
 
@@ -662,16 +667,68 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
                                                    LseCensus &cen, KC32 *__restrict__ c32 = nullptr,
                                                    const CoefM *__restrict__ cmv = nullptr,
                                                    const CoefM8 *__restrict__ cmv8 = nullptr,
-                                                   Stage stg = {}) {
+                                                   Stage stg = {}, float env_cmax = 0.0f,
+                                                   float env_amin = 0.0f, int probe = -1) {
   const int lane = threadIdx.x & 63;
   const int nch = (nb + kChunk - 1) / kChunk;
   const double *tb = reinterpret_cast<const double *>(cv);
+  // Live-range search (wave tiles, tables with envelope extremes, MixInfo):
+  // every block but the probe's whose envelope bound reaches thr lies within
+  // H = sqrt((cmax - thr) / amin) of the window [lo, hi] (its bound is at
+  // most cmax - amin d^2).  The blocks' mu' ranges are sorted, so one coarse
+  // round -- lane l tests block l S, S = ceil(blocks / 64) -- brackets the
+  // blocks whose range meets [lo - H, hi + H]: passes 1 and 2 take only the
+  // rounds covering them, and the probe's block (the prior, sigma =
+  // prior_sigma: live for every wave, in the middle of the table) is tested
+  // and summed on its own when it lies outside them.  (Config 4: pass 1 over
+  // ~4 rounds instead of 20, pass 2 no longer spans the rounds between the
+  // window and the prior.)
+  int rbeg = c0, rend = nch;  // pass-1 rounds [rbeg, rend) (chunk indices)
+  int pbk = -1;               // the probe's block, when outside those rounds
+  if constexpr (STRIDE == 1) {
+    if (env_amin > 0.0f && win.thr > -INFINITY && env_cmax < INFINITY) {
+      const float h2 = fmaxf(0.0f, (env_cmax - win.thr) / env_amin);
+      const float H = __builtin_sqrtf(h2) * 1.0001f + 1.0e-6f;  // (rounded outward)
+      const float L = win.lo - H, R = win.hi + H;
+      const int nblk = (nb + kGroup - 1) / kGroup, S = (nblk + 63) / 64;
+      const int bq = lane * S;
+      bool f = false, g = false;
+      if (bq < nblk) {
+        const float4 e = block_env<STG>(tb, stg, bq * kGroup);
+        f = e.y >= L;  // (monotone in the block: a suffix of the lanes)
+        g = e.x <= R;  //                           (a prefix)
+      }
+      const uint64_t mf = __ballot(f), mg = __ballot(g);
+      // first block that can meet [L, R]: after the last tested block left of
+      // L (the blocks past the last tested one are untested: a lane beyond
+      // it stands for them); last: before the first tested block right of R
+      // (none when block 0 already is)
+      const int lastlane = (nblk - 1) / S;
+      const int j1 = mf ? __builtin_ctzll(mf) : lastlane + 1;
+      const int bfirst = j1 == 0 ? 0 : (j1 - 1) * S + 1;
+      const int blast = mg ? min(nblk - 1, (64 - __builtin_clzll(mg)) * S - 1) : -1;
+      if (bfirst > blast) {
+        rbeg = rend = 0;
+      } else {
+        rbeg = (bfirst >> 1) & ~31;
+        rend = min(nch, ((blast >> 1) & ~31) + 32);
+      }
+      const int pb = probe >= 0 ? probe / kGroup : -1;
+      if (pb >= 0 && ((pb >> 1) < rbeg || (pb >> 1) >= rend)) pbk = pb;
+    }
+  }
   // pass 1: the largest live block bound of the wave's chunks, and the block
   // (and the first and last round with a live block: pass 2, whose
   // threshold is only ever tightened, has no live block outside them)
   float bmax = -INFINITY;
   int barg = -1, rf = -1, rl = -1;
-  for (int r0 = c0; r0 < nch; r0 += STRIDE * 32) {
+  bool probe_live = false;
+  if (pbk >= 0) {  // (every lane: a wave-uniform test)
+    const float b = envelope_bound(block_env<STG>(tb, stg, pbk * kGroup), win);
+    probe_live = b >= win.thr;
+    if (probe_live && lane == 0) { bmax = b; barg = pbk * kGroup; }
+  }
+  for (int r0 = rbeg; r0 < rend; r0 += STRIDE * 32) {
     const int k0 = round_k<STRIDE>(r0, lane);
     bool lv = false;
     if (r0 + STRIDE * (lane >> 1) < nch && k0 < nb) {
@@ -763,8 +820,9 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
 #pragma unroll
     for (int r = 0; r < KR; ++r) s[r] = 0.0;
     // the rounds pass 1 found live (every round in census builds, whose
-    // totals count the skipped blocks too)
-    const int rb = CENSUS ? c0 : rf, re = CENSUS ? nch : rl + 1;
+    // totals count the skipped blocks too; none when only the probe's block
+    // is live)
+    const int rb = CENSUS ? c0 : (rf < 0 ? 0 : rf), re = CENSUS ? nch : rl + 1;
     for (int r0 = rb; r0 < re; r0 += STRIDE * 32) {
       const int k0 = round_k<STRIDE>(r0, lane);
       const bool has = r0 + STRIDE * (lane >> 1) < nch && k0 < nb;
@@ -1062,6 +1120,15 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
           lse_fold_shifted<KR>(d, s);
         }
       }
+    }
+    // the probe's block on its own (outside the searched rounds; census
+    // builds visit every round, it is in one of them)
+    if (!CENSUS && pbk >= 0 && probe_live) {
+      CoefGroup g;
+      load_group(cs, pbk * kGroup, g);
+      float d[KR][kGroup];
+      lse_terms_shifted<KR>(g, M, y, y2, d);
+      lse_fold_shifted<KR>(d, s);
     }
     bool ok = true;
     double smax = 0.0;
@@ -1732,6 +1799,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
         const int cw0 = WT ? 0 : wv;
         bool shifted = false;
         Stage stv{};
+        stv.genv = A.coefe ? A.coefe + (mix ? sa : sb) * (A.kcap / kCoefBlock) : nullptr;
         if constexpr (STAGE) {
           stv.env = (LF4 *)(sm.stg.env + (mix ? nbb : 0));
           stv.c32 = (LC32 *)(sm.stg.c32 + (mix ? nbb : 0));
@@ -1739,6 +1807,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
         if (prune && A.lse_prune > 1 && K >= A.lse_shift_min && win.thr > -INFINITY) {
           // (the moment table of the launch's width: CoefM chunks or CoefM8 blocks)
           const int64_t ms = mix ? sa : sb;
+          const MixInfo &mi = mix ? ia : ib;
           // (two-row wave tiles only: the one-row tiles of <= 2^18 candidates
           // -- config 3 -- are bound by per-wave latency, 0.5 live blocks per
           // wave, and the form's eligibility loads only add to it: 33 -> 71 us
@@ -1752,11 +1821,13 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
           if (STAGE && staged)  // (prune mode 3 only: the staged blocks are Coef32)
             shifted = lse_chunks_shifted<KR, CENSUS, ST, true, STAGE, MW>(
                 uniform_ptr(cm), cm, cw0, K, y, valid, lacc[mix], win, nvalid, lcen,
-                uniform_ptr32(A.coef32 + ms * (A.kcap / kCoefBlock)), mt16, mt8, stv);
+                uniform_ptr32(A.coef32 + ms * (A.kcap / kCoefBlock)), mt16, mt8, stv,
+                mi.env_cmax, mi.env_amin, mi.probe);
           else if (A.lse_prune > 2)  // block-local fp32 pairs (Coef32), moment chunks (CoefM / 8)
             shifted = lse_chunks_shifted<KR, CENSUS, ST, true, false, MW>(
                 uniform_ptr(cm), cm, cw0, K, y, valid, lacc[mix], win, nvalid, lcen,
-                uniform_ptr32(A.coef32 + ms * (A.kcap / kCoefBlock)), mt16, mt8);
+                uniform_ptr32(A.coef32 + ms * (A.kcap / kCoefBlock)), mt16, mt8, stv,
+                mi.env_cmax, mi.env_amin, mi.probe);
           else
             shifted = lse_chunks_shifted<KR, CENSUS, ST>(uniform_ptr(cm), cm, cw0, K, y, valid,
                                                          lacc[mix], win, nvalid, lcen);
@@ -1779,10 +1850,10 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
             else if (A.lse_prune > 2 || A.lse_f32)  // block-local fp32 (Coef32) where the block allows it
               lse_chunks<KR, CENSUS, 1, true>(
                   uniform_ptr(cm), cm, 0, K, y, lacc[mix], prune, win, nvalid, lcen,
-                  uniform_ptr32(A.coef32 + (mix ? sa : sb) * (A.kcap / kCoefBlock)));
+                  uniform_ptr32(A.coef32 + (mix ? sa : sb) * (A.kcap / kCoefBlock)), stv);
             else
               lse_chunks<KR, CENSUS, 1>(uniform_ptr(cm), cm, 0, K, y, lacc[mix], prune, win,
-                                        nvalid, lcen);
+                                        nvalid, lcen, nullptr, stv);
           } else if (A.lse_prune > 2 || A.lse_f32) {
             lse_chunks<KR, CENSUS, kWaves, true>(
                 uniform_ptr(cm), cm, wv, K, y, lacc[mix], prune, win, nvalid, lcen,
