@@ -445,7 +445,7 @@ def main():
     plan.census(True)
     for i in range(n_prof):
         step(args.warmup + args.steps + n_prof + i)
-    census = plan.census(False, n=11)
+    census = plan.census(False, n=12)
 
     e2e = None
     if rank == 0 and world == 1 and not args.no_e2e:
@@ -494,13 +494,15 @@ def report(args, C, eng, world, mode, elapsed, value, pairs_step, pairs_suggest,
     lse_exact32 = census[6] / per_launch if census[3] else 0.0  # fp32 per-group-lift form
     lse_mom = census[9] / per_launch if census[3] else 0.0      # of lse_shift: moment form
     lse_mom8 = census[10] / per_launch if census[3] else 0.0    # of lse_mom: the 8-wide form
+    lse_momh = census[11] / per_launch if census[3] else 0.0    # of lse_mom: 16-wide degree 15
     erf_exec = census[2] / per_launch
     t_kernel = score_ms * 1e-3
     # each evaluated pair priced at the register-only rate of the arithmetic
     # it ran: per-group-max lift, one wave exponent, or quantized erf
     t_peak = ((lse_exec - lse_shift - lse_exact32) / lse_peak_exact +
-              (lse_shift - lse_mom) / lse_peak_shift + (lse_mom - lse_mom8) / lse_peak_mom +
-              lse_mom8 / lse_peak_mom8 +
+              (lse_shift - lse_mom) / lse_peak_shift +
+              (lse_mom - lse_mom8 - lse_momh) / lse_peak_mom + lse_mom8 / lse_peak_mom8 +
+              lse_momh / (2.0 * lse_peak_mom8) +
               lse_exact32 / lse_peak_exact32 + erf_exec / erf_peak)
     frac = t_peak / t_kernel if t_kernel else None
     achieved = (frac or 0.0) * lse_peak
@@ -546,11 +548,13 @@ def report(args, C, eng, world, mode, elapsed, value, pairs_step, pairs_suggest,
                      'lift; mode 3 moment form of a 16-component equal-sigma chunk: one exp2 + '
                      'a degree-9 packed fp32 polynomial per candidate and chunk, 16 pairs; '
                      '8-wide moment form of a block of 8: the same with a degree-15 polynomial, '
-                     '8 pairs; exp_issue_frac = v_exp_f32 issued / (exp_f32 peak x launch time); '
+                     '8 pairs (a 16-component chunk in degree 15: the same arithmetic, 16 pairs, '
+                     'priced at twice that peak); exp_issue_frac = v_exp_f32 issued / (exp_f32 peak x launch time); '
                      'quantized pair: 2 OCML fp64 erf + 8 flops)',
                 lse_evaluated_shifted_pairs_per_launch=lse_shift,
                 lse_evaluated_moment_pairs_per_launch=lse_mom,
                 lse_evaluated_moment8_pairs_per_launch=lse_mom8,
+                lse_evaluated_moment16_deg15_pairs_per_launch=lse_momh,
                 lse_pair_moment_peak_per_s=lse_peak_mom,
                 lse_pair_moment8_peak_per_s=lse_peak_mom8,
                 exp_issue_frac=exp_issue_frac, exp_issued_per_launch=exp_issued,

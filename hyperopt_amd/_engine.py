@@ -424,7 +424,8 @@ class Plan(object):
 
     def table(self, hp, side=0, which=2):
         """Raw scoring table of slot (hp, side) as bytes (tpe_plan_get_table:
-        0 coefficients, 1 block-local fp32, 2 moment chunks; diagnostics)."""
+        0 coefficients, 1 block-local fp32, 2 moment chunks, 3 8-wide moment
+        blocks, 4 degree-15 moment chunks; diagnostics)."""
         e = self.engine
         n = C.c_int64(0)
         with e.lock:
@@ -563,12 +564,12 @@ class Plan(object):
         one-exponent pairs re-evaluated by a wave's second attempt,
         one-exponent pairs of wide blocks (mode 3's fp64 loop), one-exponent
         pairs evaluated in the moment form of their chunk, of those the
-        8-wide form]) -- the first ``n`` (7 .. 11); enable it for the
-        following suggests."""
-        if not 0 <= n <= 11:
-            raise ValueError('the census has 11 counters')
+        8-wide form, of those the 16-wide degree-15 form]) -- the first
+        ``n`` (7 .. 12); enable it for the following suggests."""
+        if not 0 <= n <= 12:
+            raise ValueError('the census has 12 counters')
         e = self.engine
-        out = (C.c_int64 * 11)()
+        out = (C.c_int64 * 12)()
         with e.lock:
             e.check(e.lib.tpe_plan_census_n(self.p, int(bool(enable)), out, int(n)))
         return tuple(int(v) for v in out[:n])

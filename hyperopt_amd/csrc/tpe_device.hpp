@@ -292,51 +292,6 @@ __device__ __forceinline__ double row16_sum(double v) {
   return v + dppd<kDppMirror>(v);
 }
 
-// The moment form (CoefM, tpe_internal.hpp) of the 16-component chunk held
-// by this lane's DPP row (component k = lane's, k & 15 = its place in the
-// chunk): centre = mu' midpoint, T_k = t_k(centre) = c - a^2 d_k^2,
-// rho_k = 2^(T_k - T*), q_k = 2 a^2 ln2 d_k, m_j = sum_k rho_k q_k^j / j! in
-// fp64, stored fp32.  Eligible only when every valid component has the same
-// a^2 (the same sigma) and the terms are finite; else xh = +inf.
-__device__ __forceinline__ void store_lse_moments(CoefM *tm, int64_t k, EnvTerm e, bool valid) {
-  const double LN2 = 0.6931471805599453;
-  const double lo = row16_min(valid ? e.m : INFINITY), hi = row16_max(valid ? e.m : -INFINITY);
-  const double amin = row16_min(valid ? e.a2 : INFINITY), amax = row16_max(valid ? e.a2 : -INFINITY);
-  const double cen = lo <= hi ? 0.5 * (lo + hi) : 0.0;
-  const double d = valid ? e.m - cen : 0.0;
-  const double T = valid ? e.c - e.a2 * (d * d) : -INFINITY;
-  const double Tm = row16_max(T == T ? T : INFINITY);
-  const double hh = row16_max(valid ? fabs(d) : 0.0);
-  const bool ok = lo <= hi && amin == amax && amin > 0.0 && amin < 1.0e300 && Tm > -1.0e300 &&
-                  Tm < 1.0e300 && hh < 1.0e300;
-  const double rho = (valid && ok) ? exp2(T - Tm) : 0.0;
-  const double q = 2.0 * amin * LN2 * d;
-  float m[kMomDeg + 1];
-  double p = rho, fact = 1.0;
-#pragma unroll
-  for (int j = 0; j <= kMomDeg; ++j) {
-    if (j > 0) fact *= (double)j;
-    m[j] = (float)(row16_sum(p) / fact);
-    p *= q;
-  }
-  if (k % kMomChunk) return;
-  CoefM *b = tm + k / kMomChunk;
-  const double base = ok ? floor(Tm) : 0.0;
-  float xh = INFINITY;
-  if (ok) {
-    const double x = hh * 2.0 * amin * LN2;
-    xh = (float)x;
-    if ((double)xh < x) xh = nextafterf(xh, INFINITY);
-  }
-  b->center = cen;
-  b->xh = xh;
-  b->base = (float)base;
-  b->cm = (float)(Tm - base);
-  b->gam = (float)(-amin);
-#pragma unroll
-  for (int j = 0; j <= kMomDeg; ++j) b->m[j] = m[j];
-}
-
 // reductions over the 8 lanes of a coefficient block (lane & 7; all 8 active)
 __device__ __forceinline__ double row8_min(double v) {
   v = fmin(v, dppd<kDppXor1>(v));
@@ -353,34 +308,49 @@ __device__ __forceinline__ double row8_sum(double v) {
   v += dppd<kDppXor2>(v);
   return v + dppd<kDppHalfMirror>(v);
 }
+template <int CH> __device__ __forceinline__ double rowc_min(double v) {
+  return CH == 8 ? row8_min(v) : row16_min(v);
+}
+template <int CH> __device__ __forceinline__ double rowc_max(double v) {
+  return CH == 8 ? row8_max(v) : row16_max(v);
+}
+template <int CH> __device__ __forceinline__ double rowc_sum(double v) {
+  return CH == 8 ? row8_sum(v) : row16_sum(v);
+}
 
-// The 8-wide moment form (CoefM8, tpe_internal.hpp) of the coefficient block
-// held by this lane's 8-lane group: the same quantities as store_lse_moments
-// over the block's 8 components (centre = the block's mu' midpoint, as
-// store_lse_envelope's Coef32 centre), degree kMom8Deg.
-__device__ __forceinline__ void store_lse_moments8(CoefM8 *tm, int64_t k, EnvTerm e, bool valid) {
+// The moment form (CoefM / CoefM8, tpe_internal.hpp) of the CH-component
+// chunk held by this lane's DPP row of CH lanes (component k = lane's, k % CH
+// = its place in the chunk): centre = mu' midpoint, T_k = t_k(centre) = c -
+// a^2 d_k^2, rho_k = 2^(T_k - T*), q_k = 2 a^2 ln2 d_k, m_j = sum_k rho_k
+// q_k^j / j! (j <= DEG) in fp64, stored fp32.  Eligible only when every valid
+// component has the same a^2 (the same sigma) and the terms are finite; else
+// xh = +inf.  Tables: 16 components / degree 9 (CoefM), 8 / 15 (CoefM8) and
+// 16 / 15 (CoefM8 layout: the wide-window form of 16-wide plans).
+template <int CH, int DEG, typename TB>
+__device__ __forceinline__ void store_lse_moments_t(TB *tm, int64_t k, EnvTerm e, bool valid) {
   const double LN2 = 0.6931471805599453;
-  const double lo = row8_min(valid ? e.m : INFINITY), hi = row8_max(valid ? e.m : -INFINITY);
-  const double amin = row8_min(valid ? e.a2 : INFINITY), amax = row8_max(valid ? e.a2 : -INFINITY);
+  const double lo = rowc_min<CH>(valid ? e.m : INFINITY), hi = rowc_max<CH>(valid ? e.m : -INFINITY);
+  const double amin = rowc_min<CH>(valid ? e.a2 : INFINITY);
+  const double amax = rowc_max<CH>(valid ? e.a2 : -INFINITY);
   const double cen = lo <= hi ? 0.5 * (lo + hi) : 0.0;
   const double d = valid ? e.m - cen : 0.0;
   const double T = valid ? e.c - e.a2 * (d * d) : -INFINITY;
-  const double Tm = row8_max(T == T ? T : INFINITY);
-  const double hh = row8_max(valid ? fabs(d) : 0.0);
+  const double Tm = rowc_max<CH>(T == T ? T : INFINITY);
+  const double hh = rowc_max<CH>(valid ? fabs(d) : 0.0);
   const bool ok = lo <= hi && amin == amax && amin > 0.0 && amin < 1.0e300 && Tm > -1.0e300 &&
                   Tm < 1.0e300 && hh < 1.0e300;
   const double rho = (valid && ok) ? exp2(T - Tm) : 0.0;
   const double q = 2.0 * amin * LN2 * d;
-  float m[kMom8Deg + 1];
+  float m[DEG + 1];
   double p = rho, fact = 1.0;
 #pragma unroll
-  for (int j = 0; j <= kMom8Deg; ++j) {
+  for (int j = 0; j <= DEG; ++j) {
     if (j > 0) fact *= (double)j;
-    m[j] = (float)(row8_sum(p) / fact);
+    m[j] = (float)(rowc_sum<CH>(p) / fact);
     p *= q;
   }
-  if (k % kCoefBlock) return;
-  CoefM8 *b = tm + k / kCoefBlock;
+  if (k % CH) return;
+  TB *b = tm + k / CH;
   const double base = ok ? floor(Tm) : 0.0;
   float xh = INFINITY;
   if (ok) {
@@ -394,7 +364,16 @@ __device__ __forceinline__ void store_lse_moments8(CoefM8 *tm, int64_t k, EnvTer
   b->cm = (float)(Tm - base);
   b->gam = (float)(-amin);
 #pragma unroll
-  for (int j = 0; j <= kMom8Deg; ++j) b->m[j] = m[j];
+  for (int j = 0; j <= DEG; ++j) b->m[j] = m[j];
+}
+__device__ __forceinline__ void store_lse_moments(CoefM *tm, int64_t k, EnvTerm e, bool valid) {
+  store_lse_moments_t<kMomChunk, kMomDeg>(tm, k, e, valid);
+}
+__device__ __forceinline__ void store_lse_moments8(CoefM8 *tm, int64_t k, EnvTerm e, bool valid) {
+  store_lse_moments_t<kCoefBlock, kMom8Deg>(tm, k, e, valid);
+}
+__device__ __forceinline__ void store_lse_moments16h(CoefM8 *tm, int64_t k, EnvTerm e, bool valid) {
+  store_lse_moments_t<kMomChunk, kMom8Deg>(tm, k, e, valid);
 }
 
 // Natural log of a finite x > 0 in ~30 VALU (OCML's fp64 log is ~70: its

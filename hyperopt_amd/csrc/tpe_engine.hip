@@ -95,6 +95,14 @@ static bool side_streams_on() {
   return on;
 }
 static bool moment_on();
+// TPE_MOMENT_H=0: 16-wide plans without the degree-15 chunk table (A/B)
+static bool moment_h_on() {
+  static const bool on = [] {
+    const char *e = std::getenv("TPE_MOMENT_H");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
 constexpr int64_t kSmallSortMin = 2048;  // candidates per chunk worth bucketing a small draw
 
 struct tpe_engine {
@@ -134,6 +142,7 @@ struct tpe_plan {
   CoefM *d_coefm = nullptr;    // [2P][mom_stride(kcap)] moment form of 16-component chunks
   CoefM8 *d_coefm8 = nullptr;  // [2P][kcap / kCoefBlock] moment form of 8-component blocks
   float4 *d_coefe = nullptr;   // [2P][kcap / kCoefBlock] compact log-sum-exp block envelopes
+  CoefM8 *d_coefmh = nullptr;  // [2P][mom_stride(kcap)] degree-15 form of 16-component chunks
   std::vector<double> act_frac;  // per hp: expected share of the trials it is active in
   int64_t n = 0;  // history length
   // suggestion state
@@ -204,6 +213,8 @@ struct tpe_plan {
   bool graph_ok = false, pending = false;
   bool capturing = false;  // enqueue_step under graph capture (no per-call patch of score seeds)
   int32_t mom_w = 0;       // moment table the last fit wrote: 16 (CoefM), 8 (CoefM8), 0 none
+  bool mom_h = false;      // ... and with 16, the degree-15 table (CoefMH)
+  bool graph_mom_h = false;
   int32_t graph_mom_w = 0; // ... the captured graph's fit (launch_step restores it)
   HistPatch pend{};        // a small history update not yet on the device: the next
   bool has_pend = false;   // fit writes it (k_fit's patch), anything else flushes it
@@ -264,7 +275,7 @@ void plan_free_buffers(tpe_plan *p) {
                   p->d_msig, p->d_scratch, p->d_info, p->d_coef, p->d_results, p->d_seeds,
                   p->d_partial, p->d_ext, p->d_lb, p->d_la, p->d_cand, p->d_cpos,
                   p->d_ticket, p->d_sortbuf, p->d_census, p->d_lat_info, p->d_lat, p->d_coef32, p->d_coefm,
-                  p->d_coefm8, p->d_coefe};
+                  p->d_coefm8, p->d_coefe, p->d_coefmh};
   for (void *b : bufs) dfree(b);
   if (p->h_results) (void)hipHostFree(p->h_results);
   p->h_results = nullptr;
@@ -447,6 +458,7 @@ int plan_build(tpe_engine *h, const tpe_space *sp, int64_t max_trials, tpe_plan 
   CKH(dalloc(&p->d_coefm, (size_t)slots * mom_stride(kcap)));
   CKH(dalloc(&p->d_coefm8, (size_t)slots * (kcap / kCoefBlock)));
   CKH(dalloc(&p->d_coefe, (size_t)slots * (kcap / kCoefBlock)));
+  CKH(dalloc(&p->d_coefmh, (size_t)slots * mom_stride(kcap)));
   // expected activity of every hp (mom_width): an hp conditioned on branch b
   // of a categorical parent is active in ~1 / upper of the parent's trials
   // (levels are in dependency order: parents first)
@@ -653,6 +665,7 @@ ScoreArgs base_args(tpe_plan *p, int64_t n_sug) {
   a.coef32 = p->d_coef32;
   a.coefm = p->d_coefm;
   a.coefm8 = p->d_coefm8;
+  a.coefmh = p->d_coefmh;
   a.coefe = p->d_coefe;
   a.mw = p->d_mw;
   a.mmu = p->d_mmu;
@@ -668,6 +681,7 @@ ScoreArgs base_args(tpe_plan *p, int64_t n_sug) {
   a.lat_info = p->d_lat_info;
   a.lat = p->d_lat;
   a.lse_mom = p->mom_w;
+  a.lse_momh = p->mom_w == 16 && p->mom_h ? 1 : 0;
   a.l2_warm = l2_warm_on() ? 1 : 0;
   return a;
 }
@@ -716,6 +730,8 @@ FitArgs fit_args(tpe_plan *p, int32_t n_below, double prior_weight, int32_t lf, 
   a.coef32 = p->d_coef32;
   a.coefm = p->mom_w == 16 ? p->d_coefm : nullptr;
   a.coefm8 = p->mom_w == 8 ? p->d_coefm8 : nullptr;
+  a.coefmh = p->mom_w == 16 && moment_h_on() ? p->d_coefmh : nullptr;
+  p->mom_h = a.coefmh != nullptr;
   a.coefe = p->d_coefe;
   a.kcap = p->kcap;
   a.ob = p->d_scratch;
@@ -1442,6 +1458,7 @@ int tpe_score(tpe_handle_t h, int32_t family, const double *x, int64_t n, const 
   CKH(launch_prep(p->d_hps, 1, p->d_mw, p->d_mmu, p->d_msig, p->d_info, p->d_coef, p->d_coef32,
                   p->d_coefm, nullptr, p->d_coefe, p->kcap, p->d_scratch, h->stream));
   p->mom_w = moment_on() ? 16 : 0;
+  p->mom_h = false;
   rc = ensure_ext(h, p, n);
   if (rc) return rc;
   CKH(hipMemcpyAsync(p->d_ext, x, n * 8, hipMemcpyHostToDevice, h->stream));
@@ -1491,6 +1508,7 @@ int tpe_sample(tpe_handle_t h, int32_t family, const double *w, const double *mu
   CKH(launch_prep(p->d_hps, 1, p->d_mw, p->d_mmu, p->d_msig, p->d_info, p->d_coef, p->d_coef32,
                   p->d_coefm, nullptr, p->d_coefe, p->kcap, p->d_scratch, h->stream));
   p->mom_w = moment_on() ? 16 : 0;
+  p->mom_h = false;
   rc = ensure_ext(h, p, n);
   if (rc) return rc;
   CKH(launch_sample(p->d_hps, p->d_mw, p->d_mmu, p->d_msig, p->d_info, seed, stream, offset, n,
@@ -1635,7 +1653,7 @@ int tpe_plan_get_table(tpe_plan_t p, int32_t hp, int32_t side, int32_t which, vo
                        int64_t cap_bytes, int64_t *bytes) {
   if (!p || !bytes) return TPE_E_INVALID;
   tpe_engine *h = p->eng;
-  if (hp < 0 || hp >= p->P || side < 0 || side > 1 || which < 0 || which > 3)
+  if (hp < 0 || hp >= p->P || side < 0 || side > 1 || which < 0 || which > 4)
     return fail(h, TPE_E_INVALID, "bad hp/side/table");
   CKH(hipSetDevice(h->device));
   CKH(hipDeviceSynchronize());
@@ -1650,9 +1668,12 @@ int tpe_plan_get_table(tpe_plan_t p, int32_t hp, int32_t side, int32_t which, vo
   } else if (which == 2) {
     *bytes = mom_stride(p->kcap) * (int64_t)sizeof(CoefM);
     src = p->d_coefm + slot * mom_stride(p->kcap);
-  } else {
+  } else if (which == 3) {
     *bytes = p->kcap / kCoefBlock * (int64_t)sizeof(CoefM8);
     src = p->d_coefm8 + slot * (p->kcap / kCoefBlock);
+  } else {
+    *bytes = mom_stride(p->kcap) * (int64_t)sizeof(CoefM8);
+    src = p->d_coefmh + slot * mom_stride(p->kcap);
   }
   if (!out) return TPE_OK;
   if (*bytes > cap_bytes) return fail(h, TPE_E_INVALID, "capacity too small");
@@ -1742,6 +1763,7 @@ int capture_step(tpe_engine *h, tpe_plan *p, int32_t nb, double prior_weight, in
   }
   p->graph = g;
   p->graph_mom_w = p->mom_w;  // the table the captured fit writes (its args are fixed)
+  p->graph_mom_h = p->mom_h;
   CKH(hipGraphInstantiate(&p->graph_exec, g, nullptr, nullptr, 0));
   size_t nn = 0;
   CKH(hipGraphGetNodes(g, nullptr, &nn));
@@ -1810,6 +1832,7 @@ int launch_step(tpe_engine *h, tpe_plan *p, int32_t nb, const uint64_t *seeds, i
   CKH(hipGraphLaunch(p->graph_exec, st));
   p->last_nb = nb;
   p->mom_w = p->graph_mom_w;  // (no fit_args on replay: the captured fit's table)
+  p->mom_h = p->graph_mom_h;
   return TPE_OK;
 }
 

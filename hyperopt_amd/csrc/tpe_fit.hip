@@ -810,7 +810,8 @@ __device__ __forceinline__ Split compute_split(const FitArgs &A, const FitCtx &C
 // padding components of the last block (alpha = -inf: terms exactly 0).
 // ------------------------------------------------------------------------
 __device__ __forceinline__ void store_table(const tpe_hp &H, Coef *cf, Coef32 *cf32, CoefM *cfm,
-                                            CoefM8 *cfm8, float4 *cfe, int K, const double *w,
+                                            CoefM8 *cfm8, CoefM8 *cfmh, float4 *cfe, int K,
+                                            const double *w,
                                             const double *mu, const double *sg, double pacc,
                                             bool quant) {
   const int kp = (K + kCoefBlock - 1) / kCoefBlock * kCoefBlock;
@@ -820,7 +821,7 @@ __device__ __forceinline__ void store_table(const tpe_hp &H, Coef *cf, Coef32 *c
   // the 16 lanes of a moment chunk likewise (lanes past kp are padding of
   // the chunk only, with no coefficient entry)
   // (cfm null: the moment table is not wanted by this fit's suggest)
-  for (int k = threadIdx.x; k < (quant ? K : cfm ? kp16 : kp); k += blockDim.x) {
+  for (int k = threadIdx.x; k < (quant ? K : (cfm || cfmh) ? kp16 : kp); k += blockDim.x) {
     EnvTerm e{0.0, 0.0, 0.0};
     const bool real = k < K;
     const Coef c = real ? make_coef(H, w[k], mu[k], sg[k], pacc, &e)
@@ -831,6 +832,7 @@ __device__ __forceinline__ void store_table(const tpe_hp &H, Coef *cf, Coef32 *c
       if (!quant && cfm8) store_lse_moments8(cfm8, k, e, real);
     }
     if (!quant && cfm) store_lse_moments(cfm, k, e, real);
+    if (!quant && cfmh) store_lse_moments16h(cfmh, k, e, real);
   }
 }
 
@@ -910,7 +912,7 @@ __device__ __forceinline__ void prep_slot(const tpe_hp *Hg, int64_t slot, int K,
   }
   STAMP(8);
   const bool quant = (H.flags & TPE_HAS_Q) != 0;
-  store_table(H, cf, cf32, cfm, cfm8, cfe, K, w, mu, sg, pacc, quant);
+  store_table(H, cf, cf32, cfm, cfm8, nullptr, cfe, K, w, mu, sg, pacc, quant);
   if (threadIdx.x == 0) {
     MixInfo mi;
     mi.K = K; mi.kind = quant ? 1 : 0; mi.p_accept = pacc; mi.log_pacc = log(pacc);
@@ -1013,10 +1015,11 @@ __device__ __forceinline__ void fit_continuous(const FitArgs &A, const FitCtx &C
   Coef32 *cf32 = A.coef32 + slot * (A.kcap / kCoefBlock);
   CoefM *cfm = A.coefm ? A.coefm + slot * mom_stride(A.kcap) : nullptr;
   CoefM8 *cfm8 = A.coefm8 ? A.coefm8 + slot * (A.kcap / kCoefBlock) : nullptr;
+  CoefM8 *cfmh = A.coefmh ? A.coefmh + slot * mom_stride(A.kcap) : nullptr;
   float4 *cfe = A.coefe ? A.coefe + slot * (A.kcap / kCoefBlock) : nullptr;
   if (MIXLDS)
     for (int k = threadIdx.x; k < K; k += blockDim.x) { gw[k] = w[k]; gm[k] = mu[k]; gs[k] = sg[k]; }
-  store_table(H, cf, cf32, cfm, cfm8, cfe, K, w, mu, sg, pacc, quant);
+  store_table(H, cf, cf32, cfm, cfm8, cfmh, cfe, K, w, mu, sg, pacc, quant);
   // (block-uniform: K, quant)
   const float2 ex = (!quant && K >= kRangeMinK) ? envelope_extremes(cf, K, pos, sm)
                                                 : make_float2(0.0f, 0.0f);

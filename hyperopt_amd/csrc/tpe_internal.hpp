@@ -116,8 +116,8 @@ constexpr float kLseDeadBase = 26.0f;
 // second attempt (re-centred exponent) / one-exponent pairs of wide blocks
 // (the fp64 loop of mode 3) / one-exponent pairs evaluated in the moment
 // form of their chunk (CoefM, 16-wide, or CoefM8, 8-wide) / of those, the
-// 8-wide ones
-constexpr int kCensus = 11;
+// 8-wide ones / of those, the 16-wide degree-15 ones (CoefMH)
+constexpr int kCensus = 12;
 
 // Per-component scoring coefficients (make_coef, tpe_device.hpp), 4 fields:
 //   LSE: x = alpha, y = beta, z = gamma (t = alpha + y'(beta + gamma y'))
@@ -230,6 +230,13 @@ struct __attribute__((aligned(128))) CoefM8 {
   float pad[8];
 };
 static_assert(sizeof(CoefM8) == 128, "two 64-B scalar loads");
+// 16-wide plans also keep the degree-15 form of every 16-component chunk
+// (CoefM8 layout, one entry per chunk: "CoefMH"), taken for the chunks the
+// degree-9 form leaves out -- waves whose candidate window is wide (sparse
+// tails of the draw), where x exceeds kMomXLim and the chunk weighs too much
+// for the weighted criterion: config 4's 12 % of evaluated pairs in the
+// block-local pair form (3.3 VALU per pair against ~0.9 for a degree-15
+// chunk of 16)
 
 struct Partial {  // == tpe_result layout
   double score;
@@ -269,6 +276,7 @@ struct ScoreArgs {
   const Coef32 *coef32;      // [2*P][kcap / kCoefBlock] block-local fp32 LSE terms
   const CoefM *coefm;        // [2*P][mom_stride] moment form of 16-component chunks
   const CoefM8 *coefm8;      // [2*P][kcap / kCoefBlock] moment form of 8-component blocks
+  const CoefM8 *coefmh;      // [2*P][mom_stride] degree-15 form of 16-component chunks
   const float4 *coefe;       // [2*P][kcap / kCoefBlock] log-sum-exp block envelopes, compact
   const double *mw, *mmu, *msig;  // [2*P][kcap] (sampler reads side 0)
   const uint64_t *seeds;     // [S]
@@ -312,6 +320,7 @@ struct ScoreArgs {
   int32_t lse_mom;           // prune mode 3 wave tiles take the moment form of eligible
                              // chunks: 16 (CoefM), 8 (CoefM8, blocks) or 0 (TPE_MOMENT=0,
                              // or no table written by the last fit)
+  int32_t lse_momh;          // with 16: the degree-15 chunk table (coefmh) is there too
   int32_t lookup_draw;       // the sorted draw leaves the lookup slots (categorical, value
                              // lattice) unwritten and the scoring tile draws them itself,
                              // for below mixtures of 1 .. kFuseTab components (lookup_inline)
@@ -353,6 +362,7 @@ struct FitArgs {
   Coef32 *coef32;            // [2P][kcap / kCoefBlock]
   CoefM *coefm;              // [2P][mom_stride(kcap)] (null: not written)
   CoefM8 *coefm8;            // [2P][kcap / kCoefBlock] (null: not written; at most one of the two)
+  CoefM8 *coefmh;            // [2P][mom_stride(kcap)] degree-15 16-wide form (with coefm)
   float4 *coefe;             // [2P][kcap / kCoefBlock] compact envelopes (store_lse_envelope)
   int64_t kcap;
   double *ob;                // [2P][kcap] scratch: observations of the slot

@@ -402,6 +402,7 @@ struct LseCensus {
   uint32_t wide;                // one-exponent pairs of wide blocks (fp64 loop, mode 3)
   uint32_t mom;                 // one-exponent pairs evaluated in the moment form (CoefM / CoefM8)
   uint32_t mom8;                // of those, in the 8-wide form (CoefM8)
+  uint32_t momh;                // of those, in the 16-wide degree-15 form (CoefMH)
 };
 
 // A block's envelope bound over the wave's candidate range [lo, hi]: the
@@ -668,7 +669,8 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
                                                    const CoefM *__restrict__ cmv = nullptr,
                                                    const CoefM8 *__restrict__ cmv8 = nullptr,
                                                    Stage stg = {}, float env_cmax = 0.0f,
-                                                   float env_amin = 0.0f, int probe = -1) {
+                                                   float env_amin = 0.0f, int probe = -1,
+                                                   const CoefM8 *__restrict__ cmvh = nullptr) {
   const int lane = threadIdx.x & 63;
   const int nch = (nb + kChunk - 1) / kChunk;
   const double *tb = reinterpret_cast<const double *>(cv);
@@ -883,7 +885,7 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
         // qualify at larger x -- and x <= kMomXCap (fp32 Horner conditioning
         // e^(2x) bounded).  8-wide (MW 8): lane l tests its own block (one
         // CoefM8 entry per block, degree kMom8Deg), the chunk is the block.
-        uint64_t cmask = 0;
+        uint64_t cmask = 0, cmaskh = 0;
         if constexpr (MW == 8) {
           bool elig = false;
           if (KR <= 2 && cmv8 && has) {
@@ -896,26 +898,41 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
           }
           cmask = __ballot(live && elig);
         } else {
+          // (with the degree-15 table, CoefMH: the chunks the degree-9 form
+          // leaves out take it when its own bound allows -- x <= kMom8XLim,
+          // or the weighted criterion at degree 15)
           const float bnd1 = __builtin_bit_cast(float, dpp<kDppXor1>(__builtin_bit_cast(int, bnd)));
-          bool elig = false;
+          bool elig = false, eligh = false;
           if (KR <= 2 && cmv && has && !(lane & 1)) {
             const CoefM *q = cmv + (r0 + (lane >> 1));
             const float cf = (float)q->center;
             const float x = fmaxf(fabsf(win.lo - cf), fabsf(win.hi - cf)) * q->xh;
-            const float l2tau = (float)(kMomDeg + 1) * __builtin_amdgcn_logf(x) +
-                                x * 1.44269504f - kMomLog2Fact;
-            elig = x <= kMomXLim || (x <= kMomXCap && l2tau + fmaxf(bnd, bnd1) <= win.thr + 1.0f);
+            const float lx = __builtin_amdgcn_logf(x), xl = x * 1.44269504f;
+            const float bb = fmaxf(bnd, bnd1);
+            const float l2tau = (float)(kMomDeg + 1) * lx + xl - kMomLog2Fact;
+            elig = x <= kMomXLim || (x <= kMomXCap && l2tau + bb <= win.thr + 1.0f);
+            if (cmvh && !elig) {
+              const float l2tauh = (float)(kMom8Deg + 1) * lx + xl - kMom8Log2Fact;
+              eligh = x <= kMom8XLim || (x <= kMomXCap && l2tauh + bb <= win.thr + 1.0f);
+            }
           }
           const uint64_t lm = __ballot(live);
           cmask = (lm | (lm >> 1)) & __ballot(elig) & kEven;
+          cmaskh = (lm | (lm >> 1)) & __ballot(eligh) & kEven;
         }
-        const uint64_t cover = MW == 8 ? cmask : cmask | (cmask << 1);
+        const uint64_t cmall = cmask | cmaskh;
+        const uint64_t cover = MW == 8 ? cmask : cmall | (cmall << 1);
         if constexpr (CENSUS) {
-          const int n = (cmask >> lane) & 1 ? min(MW == 8 ? kGroup : kMomChunk, nb - k0) : 0;
-          uint32_t mx = (uint32_t)n;
+          const int n = (cmall >> lane) & 1 ? min(MW == 8 ? kGroup : kMomChunk, nb - k0) : 0;
+          const int nh = (cmaskh >> lane) & 1 ? min(kMomChunk, nb - k0) : 0;
+          uint32_t mx = (uint32_t)n, mh = (uint32_t)nh;
 #pragma unroll
-          for (int o = 32; o > 0; o >>= 1) mx += __shfl_xor(mx, o, 64);
+          for (int o = 32; o > 0; o >>= 1) {
+            mx += __shfl_xor(mx, o, 64);
+            mh += __shfl_xor(mh, o, 64);
+          }
           cen.mom += mx * (uint32_t)nvalid;
+          cen.momh += mh * (uint32_t)nvalid;
           if (MW == 8) cen.mom8 += mx * (uint32_t)nvalid;
           if constexpr (MW != 8) {
             // (the chunk's blocks counted as evaluated whether or not both were live)
@@ -979,6 +996,40 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
             s[0] += (double)(two ? b2[0] + b2[1] : b2[0]);
           }
         } else if constexpr (KR == 2) {
+          if (cmaskh) {
+            // the degree-15 form of 16-component chunks (CoefMH), as the
+            // 8-wide loop above with a chunk index
+            KCM8 *rh = uniform_ptrm8(cmvh) + r0;
+            uint64_t cm = cmaskh;
+            bool hm = true;
+            Mom8Group g;
+            load_mom8(rh, low_bit(cm) >> 1, g);
+            while (hm) {
+              f2v a0, p0;
+              mom8_terms(g, Mf, y, a0, p0);
+              cm &= cm - 1;
+              hm = cm != 0;
+              load_mom8(rh, low_bit(cm) >> 1, g);
+              __builtin_amdgcn_sched_barrier(0);
+              float b0[2];
+              mom_sum(a0, p0, b0);
+              if (!hm) {
+#pragma unroll
+                for (int r = 0; r < KR; ++r) s[r] += (double)b0[r];
+                break;
+              }
+              f2v a1, p1;
+              mom8_terms(g, Mf, y, a1, p1);
+              cm &= cm - 1;
+              hm = cm != 0;
+              load_mom8(rh, low_bit(cm) >> 1, g);
+              __builtin_amdgcn_sched_barrier(0);
+              float b1[2];
+              mom_sum(a1, p1, b1);
+#pragma unroll
+              for (int r = 0; r < KR; ++r) s[r] += (double)(b0[r] + b1[r]);
+            }
+          }
           KCM *rm = uniform_ptrm(cmv) + r0;
           uint64_t cm = cmask;
           bool hm = cm != 0;
@@ -1745,7 +1796,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
     // wave index as a scalar: the component addresses below are wave-uniform,
     // so the coefficients come in through scalar loads (SGPR operands)
     const int wv = __builtin_amdgcn_readfirstlane(wave);
-    LseCensus lcen{0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    LseCensus lcen{0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
     int nvalid = 0;
 #pragma unroll
     for (int r = 0; r < KR; ++r) nvalid += valid[r] ? 1 : 0;
@@ -1818,16 +1869,18 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
                                   ? A.coefm + ms * mom_stride(A.kcap) : nullptr;
           const CoefM8 *mt8 = (KR == 2 && MW == 8 && A.lse_mom == 8)
                                   ? A.coefm8 + ms * (A.kcap / kCoefBlock) : nullptr;
+          const CoefM8 *mth = (KR == 2 && MW == 16 && A.lse_mom == 16 && A.lse_momh)
+                                  ? A.coefmh + ms * mom_stride(A.kcap) : nullptr;
           if (STAGE && staged)  // (prune mode 3 only: the staged blocks are Coef32)
             shifted = lse_chunks_shifted<KR, CENSUS, ST, true, STAGE, MW>(
                 uniform_ptr(cm), cm, cw0, K, y, valid, lacc[mix], win, nvalid, lcen,
                 uniform_ptr32(A.coef32 + ms * (A.kcap / kCoefBlock)), mt16, mt8, stv,
-                mi.env_cmax, mi.env_amin, mi.probe);
+                mi.env_cmax, mi.env_amin, mi.probe, mth);
           else if (A.lse_prune > 2)  // block-local fp32 pairs (Coef32), moment chunks (CoefM / 8)
             shifted = lse_chunks_shifted<KR, CENSUS, ST, true, false, MW>(
                 uniform_ptr(cm), cm, cw0, K, y, valid, lacc[mix], win, nvalid, lcen,
                 uniform_ptr32(A.coef32 + ms * (A.kcap / kCoefBlock)), mt16, mt8, stv,
-                mi.env_cmax, mi.env_amin, mi.probe);
+                mi.env_cmax, mi.env_amin, mi.probe, mth);
           else
             shifted = lse_chunks_shifted<KR, CENSUS, ST>(uniform_ptr(cm), cm, cw0, K, y, valid,
                                                          lacc[mix], win, nvalid, lcen);
@@ -1887,10 +1940,10 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
     }
     if constexpr (CENSUS && LSE) {
       // nvalid is per lane: the per-lane sums add up to the wave's pairs
-      unsigned long long c2[8] = {lcen.total, lcen.exec, lcen.shift, lcen.f32, lcen.retry,
-                                  lcen.wide, lcen.mom, lcen.mom8};
+      unsigned long long c2[9] = {lcen.total, lcen.exec, lcen.shift, lcen.f32, lcen.retry,
+                                  lcen.wide, lcen.mom, lcen.mom8, lcen.momh};
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
+      for (int q = 0; q < 9; ++q) {
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) c2[q] += __shfl_xor(c2[q], o, 64);
       }
@@ -1903,6 +1956,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
         atomicAdd(A.census + 8, c2[5]);
         atomicAdd(A.census + 9, c2[6]);
         atomicAdd(A.census + 10, c2[7]);
+        atomicAdd(A.census + 11, c2[8]);
       }
     }
     if constexpr (!WT) {

@@ -195,7 +195,9 @@ int tpe_plan_get_mixture(tpe_plan_t p, int32_t hp, int32_t side, double *w,
  * w-rows), 1: the block-local fp32 table (128 B per block of 8), 2: the
  * moment table of 16-component chunks (64 B each), 3: the 8-wide moment
  * table (128 B per block of 8; written instead of 2 for mixtures of ~1e3
- * components, the other one is then stale).  *bytes = the table's
+ * components, the other one is then stale), 4: the degree-15 copy of 2's
+ * chunks (128 B each, 3's layout; read where a wave's window is too wide
+ * for degree 9).  *bytes = the table's
  * size; out may be NULL (size query).  The layouts are internal
  * (tpe_internal.hpp) and may change between versions.                      */
 int tpe_plan_get_table(tpe_plan_t p, int32_t hp, int32_t side, int32_t which, void *out,
@@ -297,14 +299,15 @@ int tpe_plan_set_lattice(tpe_plan_t p, int32_t enable);
  * zeros; a wave's retried pass counts again) -- and switch the census on (enable != 0)
  * or off for the following suggests.  counts has 6 entries.               */
 int tpe_plan_census(tpe_plan_t p, int32_t enable, int64_t *counts);
-/* The same with n_counts entries (up to 11): [6] of [5] the log-sum-exp pairs
+/* The same with n_counts entries (up to 12): [6] of [5] the log-sum-exp pairs
  * evaluated in the block-local fp32 per-group-lift form (prune mode 3 on
  * mixtures below the one-exponent size), [7] of [4] the one-exponent pairs
  * evaluated again by a wave's second attempt (its exponent re-centred),
  * [8] of [4] the one-exponent pairs of wide blocks (mode 3's fp64 loop),
  * [9] of [4] the one-exponent pairs evaluated in the moment form of their
  * 16-component chunk (one exp2 + a degree-9 polynomial per chunk) or, [10]
- * of [9], of their 8-component block (one exp2 + a degree-15 polynomial). */
+ * of [9], of their 8-component block (one exp2 + a degree-15 polynomial),
+ * [11] of [9] the 16-component chunks read at degree 15 (table 4).         */
 int tpe_plan_census_n(tpe_plan_t p, int32_t enable, int64_t *counts, int32_t n_counts);
 
 /* Prior draws of n_suggest whole suggestions (rand.suggest, the TPE startup

@@ -640,7 +640,8 @@ def test_moment_table_vs_numpy(cfg4_plan):
     mixture: per 16-component chunk of mu-sorted components, centre = mu'
     midpoint, T_k = c_k - a^2 d_k^2, T* = max, m_j = sum_k 2^(T_k - T*) q_k^j / j!
     with q_k = 2 a^2 ln2 d_k, xh = max |q_k|; chunks whose sigmas differ (the
-    prior's) are not eligible (xh = +inf).  fp32 fields to fp32 rounding."""
+    prior's) are not eligible (xh = +inf).  The degree-15 copy (CoefMH,
+    which=4: same chunks, j <= 15) likewise.  fp32 fields to fp32 rounding."""
     dom, plan = cfg4_plan
     LOG2E, LN2 = 1.4426950408889634, math.log(2.0)
     for lab in ('x0', 'x57'):
@@ -648,6 +649,7 @@ def test_moment_table_vs_numpy(cfg4_plan):
         for side in (0, 1):
             w, mu, sg = plan.mixture(hp_i, side)
             t = plan.table(hp_i, side, 2).view(_MOM)
+            th = plan.table(hp_i, side, 4).view(_MOM8)
             K = w.size
             sgc = np.maximum(sg, 1e-12)
             from oracle import tpe_oracle as O
@@ -676,6 +678,15 @@ def test_moment_table_vs_numpy(cfg4_plan):
                 np.testing.assert_allclose(e['cm'], Ts - np.floor(Ts), atol=2e-7)
                 np.testing.assert_allclose(e['gam'], -a2_[0], rtol=1e-7)
                 np.testing.assert_allclose(e['m'], mom, rtol=2e-7, atol=1e-30)
+                # the degree-15 copy of the same chunk (CoefMH, which=4)
+                eh = th[ch]
+                momh = np.array([np.sum(rho * q ** j) / math.factorial(j) for j in range(16)])
+                assert eh['center'] == cen
+                np.testing.assert_allclose(eh['xh'], np.abs(q).max(), rtol=2e-7)
+                assert eh['base'] == np.floor(Ts)
+                np.testing.assert_allclose(eh['cm'], Ts - np.floor(Ts), atol=2e-7)
+                np.testing.assert_allclose(eh['gam'], -a2_[0], rtol=1e-7)
+                np.testing.assert_allclose(eh['m'], momh, rtol=2e-7, atol=1e-30)
             if side == 1:
                 assert n_ok >= 0.99 * (-(-K // 16)) - 1, (lab, n_ok)
 
