@@ -15,10 +15,16 @@ SQ_WAIT_* count quad-cycles; GRBM_GUI_ACTIVE is summed over the 8 XCDs):
   waves_per_simd       = 4 * SQ_WAVE_CYCLES / (SIMDs * GRBM_GUI_ACTIVE / 8)
   wait_inst_frac       = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES
   wait_any_frac        = SQ_WAIT_ANY / SQ_WAVE_CYCLES (pass B, its own waves)
+A label that names a bench config (cfg2 ... cfg5) also writes
+traffic.json[<label>]['valu_insts_per_launch']: the dispatch-weighted mean
+SQ_INSTS_VALU of its scoring launches (k_score, k_score_wave,
+k_score_wave1; census builds excluded), which bench.py turns into
+roofline.valu_per_evaluated_pair (x 64 lanes / evaluated pairs).
 usage: sq_summary.py <out.json> <label>=<dir> [<label>=<dir> ...]
 """
 import collections
 import json
+import os
 import re
 import sqlite3
 import sys
@@ -27,13 +33,13 @@ SIMDS = 256 * 4
 
 
 def short(name):
-    m = re.search(r'(k_[a-z_]+)(?:I(L[ib]\d+E)+E)?', name)
+    m = re.search(r'(k_[a-z_0-9]+?)(?:I(L[ib]\d+E)+E|$|[^a-z_0-9])', name)
     if not m:
         return None
     base = m.group(1)
     if base == 'k_score' and ('ILb0ELb1E' in name or 'ILb1ELb1E' in name):
         return base + '_census'
-    if base == 'k_score_wave' and 'ILb1E' in name:   # k_score_wave<true>: census build
+    if base.startswith('k_score_wave') and 'ILb1E' in name:   # k_score_wave<true>: census build
         return base + '_census'
     return base
 
@@ -100,6 +106,24 @@ def main(argv):
     res['_note'] = __doc__.split('usage:')[0].strip()
     with open(dst, 'w') as f:
         json.dump(res, f, indent=1, sort_keys=True)
+    tpath = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'traffic.json')
+    traffic = json.load(open(tpath)) if os.path.exists(tpath) else {}
+    for label, ks in res.items():
+        if not re.fullmatch(r'cfg\d', label):
+            continue
+        parts = []
+        for k in ('k_score', 'k_score_wave', 'k_score_wave1'):
+            e = ks.get(k, {})
+            nd = [v for n, v in e.items() if n.startswith('_dispatches')]
+            if 'SQ_INSTS_VALU' in e and nd:
+                parts.append((nd[0], e['SQ_INSTS_VALU']))
+        if parts:
+            t = traffic.setdefault(label, {})
+            t['valu_insts_per_launch'] = sum(n * v for n, v in parts) / sum(n for n, _ in parts)
+            t['_sq_source'] = '%s (SQ_INSTS_VALU, wave64 instructions per score launch)' % (
+                os.path.basename(dst))
+    with open(tpath, 'w') as f:
+        json.dump(traffic, f, indent=1, sort_keys=True)
     for label, ks in res.items():
         if label.startswith('_'):
             continue
