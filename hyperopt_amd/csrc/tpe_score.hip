@@ -945,37 +945,29 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
           }
         }
         if constexpr (MW == 8 && KR == 2) {
+          // two blocks per iteration, both loaded at its top (no group live
+          // across the back edge: a loop-carried 21-SGPR group was spilled to
+          // VGPR lanes every iteration); their fp32 sums added in fp32 and
+          // converted once (as the pair loop below).  The second of an odd
+          // last pair is block 0 of the round again, a valid address, its sum
+          // dropped.
           KCM8 *rm = uniform_ptrm8(cmv8) + 2 * r0;
           uint64_t cm = cmask;
-          bool hm = cm != 0;
-          Mom8Group g;
-          if (hm) load_mom8(rm, low_bit(cm), g);
-          // two blocks per iteration, their fp32 sums added in fp32 and
-          // converted once (as the pair loop below)
-          while (hm) {
-            f2v a0, p0;
-            mom8_terms(g, Mf, y, a0, p0);
+          while (cm) {
+            Mom8Group ga, gb;
+            load_mom8(rm, low_bit(cm), ga);
             cm &= cm - 1;
-            hm = cm != 0;
-            load_mom8(rm, low_bit(cm), g);
-            __builtin_amdgcn_sched_barrier(0);
-            float b0[2];
+            const bool two = cm != 0;
+            load_mom8(rm, low_bit(cm), gb);
+            cm &= cm - 1;
+            f2v a0, p0, a1, p1;
+            mom8_terms(ga, Mf, y, a0, p0);
+            mom8_terms(gb, Mf, y, a1, p1);
+            float b0[2], b1[2];
             mom_sum(a0, p0, b0);
-            if (!hm) {
-#pragma unroll
-              for (int r = 0; r < KR; ++r) s[r] += (double)b0[r];
-              break;
-            }
-            f2v a1, p1;
-            mom8_terms(g, Mf, y, a1, p1);
-            cm &= cm - 1;
-            hm = cm != 0;
-            load_mom8(rm, low_bit(cm), g);
-            __builtin_amdgcn_sched_barrier(0);
-            float b1[2];
             mom_sum(a1, p1, b1);
 #pragma unroll
-            for (int r = 0; r < KR; ++r) s[r] += (double)(b0[r] + b1[r]);
+            for (int r = 0; r < KR; ++r) s[r] += (double)(two ? b0[r] + b1[r] : b0[r]);
           }
         } else if constexpr (MW == 8 && KR == 1) {
           // one row: blocks in pairs (the second of an odd last pair is block
@@ -1713,13 +1705,15 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
   // component blocks) are shared out over blocks, CUs and SIMDs instead of
   // landing on one CU together.  A wave's sums depend only on its own
   // candidates: the mapping changes no result.
-  int64_t wt0 = (int64_t)tile * tile_cands(KIND) + (WT ? wave * 64 * KR : 0);
+  // (wave-uniform: a scalar, so the finalize can recompute li from it)
+  const int wvs = __builtin_amdgcn_readfirstlane(wave);
+  int64_t wt0 = (int64_t)tile * tile_cands(KIND) + (WT ? wvs * 64 * KR : 0);
   if constexpr (kind_wave_lse(KIND)) {
     constexpr int SBB = kSortedBlock / tile_cands(KIND);  // blocks per sort block
     static_assert(SBB * tile_cands(KIND) == kSortedBlock, "blocks tile the sort block");
     const int sb = tile / SBB, q = tile % SBB;
     const int nbs = min(SBB, ntiles - sb * SBB);
-    wt0 = ((int64_t)sb * SBB * kWaves + q + (int64_t)nbs * wave) * 64 * KR;
+    wt0 = ((int64_t)sb * SBB * kWaves + q + (int64_t)nbs * wvs) * 64 * KR;
   }
 #pragma unroll
   for (int r = 0; r < KR; ++r) {
@@ -2050,8 +2044,18 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
   } else
 #pragma unroll
   for (int r = 0; r < KR; ++r) {
+    // log-sum-exp wave tiles recompute their slots from the scalar wt0 and
+    // read their candidate again here rather than keeping either in
+    // registers through the component loops (memory is stable during the
+    // launch: DESIGN §3)
+    if constexpr (LSE && WT && !TDRAW) {
+      const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+      li[r] = wt0 + r * 64 + ln;
+      valid[r] = li[r] < A.n_cand;
+    }
     if (!valid[r]) continue;
     double lpb = NAN, lpa = NAN, sc;
+    if constexpr (LSE && WT && !TDRAW) x[r] = cand[li[r]];
 #ifdef TPE_REREAD3
     // (diagnostic build dbg5: the winner's value taken from a plain re-read)
     if constexpr (LSE && WT) x[r] = cand[li[r]];
