@@ -1471,6 +1471,8 @@ template <int R>
 struct ScoreSmemT {
   double2 wpart[2][kWaves][R][64];      // per-wave partials (below, above)
   double2 merged[2][R][64];             // merged per (mixture, candidate row)
+  double xs[R > 1 ? kWaves : 1][R][64];  // two-row wave tiles: each wave's candidates
+                                        //   (kept here, not in registers, till finalize)
   double best_s[kWaves], best_v[kWaves];  // wave tiles: each wave's argmax
   int64_t best_i[kWaves];
 #ifdef TPE_REREAD
@@ -1737,6 +1739,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
                                   A.msig + sb * A.kcap, seed, gi, (uint32_t)hp);
     } else {
       x[r] = valid[r] ? cand[li[r]] : (LOGN ? 1.0 : 0.0);
+      if constexpr (LSE && WT && KR > 1) sm.xs[wave][r][lane] = x[r];
     }
     y[r] = ub[r] = lb[r] = 0.0;
     // candidate-side transforms, once per candidate
@@ -2044,18 +2047,18 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
   } else
 #pragma unroll
   for (int r = 0; r < KR; ++r) {
-    // log-sum-exp wave tiles recompute their slots from the scalar wt0 and
-    // read their candidate again here rather than keeping either in
-    // registers through the component loops (memory is stable during the
-    // launch: DESIGN §3)
-    if constexpr (LSE && WT && !TDRAW) {
+    // two-row log-sum-exp wave tiles recompute their slots from the scalar
+    // wt0 and take their candidates back from LDS rather than keeping either
+    // in registers through the component loops
+    if constexpr (LSE && WT && KR > 1 && !TDRAW) {
       const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
       li[r] = wt0 + r * 64 + ln;
       valid[r] = li[r] < A.n_cand;
+      asm volatile("" ::: "memory");  // (a reload, not the stored register)
+      x[r] = sm.xs[wave][r][ln];
     }
     if (!valid[r]) continue;
     double lpb = NAN, lpa = NAN, sc;
-    if constexpr (LSE && WT && !TDRAW) x[r] = cand[li[r]];
 #ifdef TPE_REREAD3
     // (diagnostic build dbg5: the winner's value taken from a plain re-read)
     if constexpr (LSE && WT) x[r] = cand[li[r]];
