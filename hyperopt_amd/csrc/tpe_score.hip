@@ -1200,10 +1200,12 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
 }
 
 // Mixtures of at most kSmallMix components on wave tiles (the good side: K_b
-// = n_below + 1 <= 26) -- an exact two-pass log-sum-exp straight from the
-// block's LDS copy of the coefficients: the lane's largest term m (the same
-// fp64 t = alpha + y'(beta + gamma y') as lse_terms), then the terms 2^(t -
-// ceil m) summed in fp32 over runs of 8 and in fp64 across them.  No envelope
+// = n_below + 1 <= 26) -- a log-sum-exp straight from the block's LDS copy
+// of the coefficients, in one pass against the mixture's peak bound mtop (the
+// same fp64 t = alpha + y'(beta + gamma y') as lse_terms); a wave with a
+// candidate far below every peak takes the two-pass form: the lane's largest
+// term m, then the terms 2^(t - ceil m) summed in fp32 over runs of 8 and in
+// fp64 across them (round 5's form, ~40% more work).  No envelope
 // round, window, scalar coefficient loads or per-group lift: the envelope /
 // fp64 lift loop these mixtures took (their blocks are wide in sigma units,
 // so never in the fp32 form) spent ~7 us per config-5 wave waiting on loads.
@@ -1212,10 +1214,46 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
 constexpr int kSmallMix = 32;
 template <int KR>
 __device__ __forceinline__ void lse_small(const double (*__restrict__ cf)[kSmallMix], int K,
-                                          const double (&y)[KR], LseAcc (&out)[KR]) {
-  double y2[KR], m[KR];
+                                          const double (&y)[KR], LseAcc (&out)[KR], double mtop) {
+  double y2[KR];
 #pragma unroll
-  for (int r = 0; r < KR; ++r) { y2[r] = y[r] * y[r]; m[r] = -INFINITY; }
+  for (int r = 0; r < KR; ++r) y2[r] = y[r] * y[r];
+  // one pass against the mixture's bound mtop (staged with the coefficients:
+  // row 3 = alpha - mtop), the terms 2^(t - mtop) <= 1 summed in fp32 over
+  // runs of 8 and in fp64 across them.  A lane whose sum comes out below
+  // 2^-60 (a candidate far below every component's peak: its terms may have
+  // flushed in fp32) sends the wave to the two-pass form below
+  if (mtop > -INFINITY && mtop < INFINITY) {
+    double sd[KR];
+    float sf[KR];
+#pragma unroll
+    for (int r = 0; r < KR; ++r) { sd[r] = 0.0; sf[r] = 0.0f; }
+    for (int k = 0; k < K; ++k) {
+      const double cx = cf[3][k], cy = cf[1][k], cz = cf[2][k];
+#pragma unroll
+      for (int r = 0; r < KR; ++r)
+        sf[r] += __builtin_amdgcn_exp2f((float)fma(cz, y2[r], fma(cy, y[r], cx)));
+      if ((k & 7) == 7) {
+#pragma unroll
+        for (int r = 0; r < KR; ++r) { sd[r] += (double)sf[r]; sf[r] = 0.0f; }
+      }
+    }
+    bool ok = true;
+#pragma unroll
+    for (int r = 0; r < KR; ++r) {
+      sd[r] += (double)sf[r];
+      ok &= !(sd[r] < 0x1p-60);  // (NaN: the lpdf is NaN either way)
+    }
+    if (__all(ok)) {
+#pragma unroll
+      for (int r = 0; r < KR; ++r)
+        out[r] = (y[r] != y[r]) ? LseAcc{NAN, NAN} : LseAcc{mtop, sd[r]};
+      return;
+    }
+  }
+  double m[KR];
+#pragma unroll
+  for (int r = 0; r < KR; ++r) m[r] = -INFINITY;
   for (int k = 0; k < K; ++k) {
     const double cx = cf[0][k], cy = cf[1][k], cz = cf[2][k];
 #pragma unroll
@@ -1479,8 +1517,10 @@ struct ScoreSmemT {
   int64_t best_li[kWaves];
 #endif
   uint32_t arrive;                      // wave tiles: waves done with the tile
-  double small[2][3][kSmallMix];        // wave tiles: mixtures of <= kSmallMix components
-                                        //   (alpha, beta, gamma rows; below, above), lse_small
+  double small[2][4][kSmallMix];        // wave tiles: mixtures of <= kSmallMix components
+                                        //   (alpha, beta, gamma, alpha - mtop rows; below,
+                                        //   above), lse_small
+  double small_m[2];                    //   mtop = ceil(max_k peak_k), the terms' bound
   DrawTableT<kFuseTab> dt;              // lookup tiles drawing their candidates (lookup_inline)
   double top_s;                         // lookup scans: the best score any value can get
   int top_nan;                          //   (a NaN score: top is NaN)
@@ -1595,15 +1635,32 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
     // small mixtures' coefficients (lse_small) into LDS: thread t of the first
     // 2 x kSmallMix copies component t % kSmallMix of mixture t / kSmallMix
     if constexpr (LSE) {
+      // (wave 0, every lane: lanes 32q .. 32q + 31 hold mixture q.  The
+      // bound mtop: every term t_k(y) is at most its peak alpha - beta^2 /
+      // (4 gamma), so 2^(t - mtop) <= 1 for any candidate -- lse_small's one
+      // pass needs no per-lane maximum)
       if (threadIdx.x < 2 * kSmallMix) {
         const int q = threadIdx.x / kSmallMix, k = threadIdx.x % kSmallMix;
         const int Kq = q ? ia.K : ib.K;
-        if (Kq <= kSmallMix && k < Kq && A.lse_prune != 0) {
+        const bool cp = Kq <= kSmallMix && k < Kq && A.lse_prune != 0;
+        double ca = 0.0, cb = 0.0, cg = 0.0, pk = -INFINITY;
+        if (cp) {
           const double *t = reinterpret_cast<const double *>(A.coef + (q ? sa : sb) * A.kcap);
-          sm.small[q][0][k] = t[coef_off(k, 0)];
-          sm.small[q][1][k] = t[coef_off(k, 1)];
-          sm.small[q][2][k] = t[coef_off(k, 2)];
+          ca = t[coef_off(k, 0)];
+          cb = t[coef_off(k, 1)];
+          cg = t[coef_off(k, 2)];
+          pk = ca - cb * cb / (4.0 * cg);
         }
+#pragma unroll
+        for (int o = kSmallMix / 2; o > 0; o >>= 1) pk = fmax(pk, __shfl_xor(pk, o, 64));
+        const double mt = ceil(pk);
+        if (cp) {
+          sm.small[q][0][k] = ca;
+          sm.small[q][1][k] = cb;
+          sm.small[q][2][k] = cg;
+          sm.small[q][3][k] = ca - mt;
+        }
+        if (k == 0) sm.small_m[q] = mt;
       }
     }
     if constexpr (STAGE) {
@@ -1822,7 +1879,7 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
         }
         if (WT && prune && K <= kSmallMix) {
           // a small mixture (the good side): the direct exact two-pass sum
-          lse_small<KR>(sm.small[mix], K, y, lacc[mix]);
+          lse_small<KR>(sm.small[mix], K, y, lacc[mix], sm.small_m[mix]);
           if constexpr (CENSUS) {
             lcen.total += (uint32_t)(K * nvalid);
             lcen.exec += (uint32_t)(K * nvalid);
