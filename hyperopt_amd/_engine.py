@@ -46,7 +46,7 @@ EXPORTS = (
 
 # include/tpe_engine.h TPE_SHARD_ALIGN: candidate splits at multiples of this
 # give byte-identical suggests (the large-draw value-bucketing block)
-SHARD_ALIGN = 4096
+SHARD_ALIGN = 8192
 
 
 class EngineUnavailable(RuntimeError):

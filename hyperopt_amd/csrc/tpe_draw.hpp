@@ -487,29 +487,37 @@ __device__ __forceinline__ uint64_t lanes_equal8(uint32_t d, bool v) {
 }
 
 template <int NW, typename Dest>
-__device__ __forceinline__ void stable_bucket_scatter(const unsigned char *bk, int n, int *cnt,
+__device__ __forceinline__ void stable_bucket_scatter(const unsigned char *bk, int n, uint32_t *cnt,
                                                       Dest dest) {
+  // counts and bases per (wave, bucket) are < 2^16 (n <= kSortedBlock): two
+  // buckets per 32-bit LDS word, bucket b in half b & 1 of word b >> 1
+  static_assert(kSortedBlock < 65536, "16-bit bucket counts");
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int per = ((n + NW * 64 - 1) / (NW * 64)) * 64;
   const int r0 = w * per, r1 = min(n, r0 + per);
-  int *mine = cnt + w * 256;
-  for (int b = lane; b < 256; b += 64) mine[b] = 0;
+  uint32_t *mine = cnt + w * (kSortBuckets / 2);
+  for (int b = lane; b < kSortBuckets / 2; b += 64) mine[b] = 0u;
   // (a wave's LDS ops complete in order: no barrier between its own rows)
   // counts: one LDS atomic per element into the wave's own bins (the order
   // of the adds does not matter; the ranks below keep the scatter stable)
   for (int base = r0; base < r1; base += 64) {
     const int i = base + lane;
-    if (i < r1)
-      __hip_atomic_fetch_add(&mine[bk[i]], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (i < r1) {
+      const unsigned d = bk[i];
+      __hip_atomic_fetch_add(&mine[d >> 1], 1u << ((d & 1) * 16), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
   }
   __syncthreads();
   // bucket b (thread b of the first 256): its total over the waves, a block
-  // scan of the totals, then the (bucket, wave) bases in place
+  // scan of the totals, then the (bucket, wave) bases in place (the even
+  // thread of each pair writes the pair's word)
   static_assert(NW * 64 >= 256, "one thread per bucket");
   __shared__ int wtot[4];
+  const int hb = (threadIdx.x & 1) * 16;
   int tot = 0;
   if (threadIdx.x < 256)
-    for (int q = 0; q < NW; ++q) tot += cnt[q * 256 + threadIdx.x];
+    for (int q = 0; q < NW; ++q) tot += (int)((cnt[q * 128 + (threadIdx.x >> 1)] >> hb) & 0xffffu);
   int x = tot;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -522,8 +530,10 @@ __device__ __forceinline__ void stable_bucket_scatter(const unsigned char *bk, i
     int acc = x - tot;
     for (int q = 0; q < w; ++q) acc += wtot[q];
     for (int q = 0; q < NW; ++q) {
-      const int c = cnt[q * 256 + threadIdx.x];
-      cnt[q * 256 + threadIdx.x] = acc;
+      const uint32_t word = cnt[q * 128 + (threadIdx.x >> 1)];
+      const int c = (int)((word >> hb) & 0xffffu);
+      const int acc1 = __shfl_xor(acc, 1, 64);  // (the pair's other bucket)
+      if (!(threadIdx.x & 1)) cnt[q * 128 + (threadIdx.x >> 1)] = (uint32_t)acc | ((uint32_t)acc1 << 16);
       acc += c;
     }
   }
@@ -534,8 +544,12 @@ __device__ __forceinline__ void stable_bucket_scatter(const unsigned char *bk, i
     const uint32_t d = v ? bk[i] : 0u;
     const uint64_t mt = lanes_equal8(d, v);
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    if (v) dest(i, mine[d] + __popcll(mt & lt));
-    if (v && lane == __ffsll((long long)mt) - 1) mine[d] += __popcll(mt);
+    const int sh = (int)(d & 1) * 16;
+    if (v) dest(i, (int)((mine[d >> 1] >> sh) & 0xffffu) + __popcll(mt & lt));
+    // (leaders of the two buckets of one word may update it together: atomic)
+    if (v && lane == __ffsll((long long)mt) - 1)
+      __hip_atomic_fetch_add(&mine[d >> 1], (uint32_t)__popcll(mt) << sh, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
   }
 }
 
@@ -554,7 +568,7 @@ struct SortedDrawLds {
   DrawTableT<CAP> T;
   double xs[kSortedBlock];          // the block's draws, in draw order
   unsigned char bk[kSortedBlock];   // their buckets
-  int32_t cnt[NT / 64 * kSortBuckets];  // stable scatter counts / bases
+  uint32_t cnt[NT / 64 * kSortBuckets / 2];  // stable scatter counts / bases (16-bit pairs)
   double red[2][NT / 64];
 };
 
@@ -583,7 +597,7 @@ __device__ __forceinline__ void sorted_block_body(const ScoreArgs &A, int slot, 
     if (tab) build_table(H, K, bw, bmu, bsg, L.T);
   }
   const uint64_t seed = suggestion_seed(A, s);
-  const int n = (int)min<int64_t>(kSortedBlock, A.n_cand - base);
+  const int n = (int)min<int64_t>((int64_t)1 << A.sort_log2, A.n_cand - base);
   const int64_t off = (int64_t)s * A.cand_sstride + (int64_t)slot * A.n_cand + base;
   double *out = const_cast<double *>(A.cand) + off;
   const int t = threadIdx.x;

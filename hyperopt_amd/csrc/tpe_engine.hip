@@ -657,6 +657,7 @@ double group_pairs(tpe_plan *p, int kind, int32_t n_slots, int64_t cn, int64_t n
 
 ScoreArgs base_args(tpe_plan *p, int64_t n_sug) {
   ScoreArgs a{};
+  a.sort_log2 = kSortLog2Small;
   a.hps = p->d_hps;
   a.cond_parent = p->d_cp;
   a.cond_branch = p->d_cb;
@@ -995,6 +996,7 @@ int run_level(tpe_engine *h, tpe_plan *p, int level, int64_t n_sug, int64_t n_ca
     for (int i = 0; i < kInlineSeeds && i < n_sug; ++i) a.seed_inline[i] = p->h_seeds[i];
     a.n_inline_seeds = (int32_t)std::min<int64_t>(n_sug, kInlineSeeds);
     a.lse_pos = (sorted_draw || small_sort) ? 1 : 0;
+    a.sort_log2 = sort_log2_for(n_total);  // (the whole suggestion's: shards agree)
     // lookup slots drawn by their scoring tiles (no write / read-back of their
     // candidates); not in a captured graph, whose replays patch the seeds of
     // the draw nodes only
@@ -1140,6 +1142,7 @@ int run_external(tpe_engine *h, tpe_plan *p, int32_t hp, const double *ext, int6
   a.force_active = 1;
   if (sorted) {
     a.cand = p->d_cand;
+    a.sort_log2 = sort_log2_for(n);
     CKH(launch_sort_ext(a, ext, p->d_cpos, st));
     a.cand_pos = p->d_cpos;
     a.lse_pos = 1;

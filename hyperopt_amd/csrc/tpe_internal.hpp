@@ -313,6 +313,7 @@ struct ScoreArgs {
   int32_t accumulate;        // merge with results of an earlier candidate chunk
   unsigned long long *census;  // optional [kCensus] pair counters (tpe_plan_census)
   int32_t lse_pos;           // LSE slots' candidates are value-bucketed (cand_pos valid)
+  int32_t sort_log2;         // their sort blocks: 1 << sort_log2 candidates (sort_log2_for)
   int32_t lse_prune;         // skip log-sum-exp blocks of exact-zero terms (needs lse_pos)
   int32_t lse_shift_min;     // lse_prune 2: smallest mixture (components) for one wave exponent
   int32_t lse_f32;           // unpruned log-sum-exp slots also take the block-local fp32
@@ -440,7 +441,17 @@ hipError_t launch_draw(const ScoreArgs &a, bool table, hipStream_t st);
 // into value buckets with their chunk positions in pos_out (tile coherence
 // for the log-sum-exp block skip and the erf dead-zone skip); small_table:
 // every below K <= kFuseTab
-constexpr int kSortedBlock = 4096;
+constexpr int kSortedBlock = TPE_SHARD_ALIGN;  // the largest sort block (LDS sizing)
+// sort blocks of a launch: 1 << ScoreArgs::sort_log2 candidates -- 8192 for
+// suggestions of > kWaveRowSplitMax candidates (two-row wave tiles: a wave's
+// 128 candidates are 1/64 of its block's value quantiles, so its window and
+// the live component blocks in it are half those of 4096-candidate blocks),
+// 4096 below (fewer, shorter draw blocks for the small launches)
+constexpr int kSortLog2Large = 13, kSortLog2Small = 12;
+static_assert((1 << kSortLog2Large) == kSortedBlock, "largest sort block");
+__host__ __device__ constexpr int sort_log2_for(int64_t n_total) {
+  return n_total > kWaveRowSplitMax ? kSortLog2Large : kSortLog2Small;
+}
 // fast: every slot the launch draws is a bounded continuous one (low and
 // high) whose below mixture fits the table, the rest lookup slots their tiles
 // draw (lookup_draw) -- the kernel without the out-of-line draws

@@ -77,31 +77,32 @@ __device__ __forceinline__ void sorted_block(const ScoreArgs &A, int32_t *__rest
   // lookup slots the scoring tile draws itself: nothing to write
   if (!EXT && (kind == KIND_CAT || kind == KIND_LAT) && lookup_inline(A, A.info[2 * hp].K)) return;
   sorted_block_body<CAP, NT, EXT, FAST>(
-      A, slot, s, (int64_t)blockIdx.x * kSortedBlock,
+      A, slot, s, (int64_t)blockIdx.x << A.sort_log2,
       kind_lse(kind) || kind == KIND_ERF_G || kind == KIND_ERF_L, kind_logn(kind), pos_out, src,
       L);
 }
 
+// (sorted draws: 512-thread blocks; an 8192-candidate block's LDS, ~78 KB
+// with the small table, leaves two blocks per CU -- four waves per SIMD)
+constexpr int kSortThreads = 512;
 template <int CAP>
-// (LDS holds three blocks per CU: three waves per SIMD is the occupancy the
-// registers must allow, <= 168 VGPRs)
-__global__ __launch_bounds__(kDrawThreads) __attribute__((amdgpu_waves_per_eu(CAP <= kFuseTab ? 3 : 1)))
+__global__ __launch_bounds__(kSortThreads) __attribute__((amdgpu_waves_per_eu(CAP <= kFuseTab ? 2 : 1)))
 void k_draw_sorted(ScoreArgs A, int32_t *__restrict__ pos_out) {
-  __shared__ SortedDrawLds<CAP, kDrawThreads> L;
-  sorted_block<CAP, kDrawThreads, false>(A, pos_out, nullptr, L);
+  __shared__ SortedDrawLds<CAP, kSortThreads> L;
+  sorted_block<CAP, kSortThreads, false>(A, pos_out, nullptr, L);
 }
 // levels whose drawn slots are all bounded continuous with a table (configs 4
 // and 5): the inline draw only (sorted_block_body FAST)
 template <int CAP>
-__global__ __launch_bounds__(kDrawThreads) __attribute__((amdgpu_waves_per_eu(CAP <= kFuseTab ? 3 : 1)))
+__global__ __launch_bounds__(kSortThreads) __attribute__((amdgpu_waves_per_eu(CAP <= kFuseTab ? 4 : 1)))
 void k_draw_sorted_fast(ScoreArgs A, int32_t *__restrict__ pos_out) {
-  __shared__ SortedDrawLds<CAP, kDrawThreads> L;
-  sorted_block<CAP, kDrawThreads, false, true>(A, pos_out, nullptr, L);
+  __shared__ SortedDrawLds<CAP, kSortThreads> L;
+  sorted_block<CAP, kSortThreads, false, true>(A, pos_out, nullptr, L);
 }
 
 // The same blocks on 1024 threads, for launches of too few blocks to fill the
-// CUs (the block's 4096 draws are split 4 x finer; the scatter is stable, so
-// the output does not depend on the block size)
+// CUs (the block's draws are split 2 x finer; the scatter is stable, so the
+// output does not depend on the block size)
 template <int CAP>
 __global__ __launch_bounds__(kWideDrawThreads) void k_draw_sorted_wide(ScoreArgs A,
                                                                        int32_t *__restrict__ pos_out) {
@@ -132,7 +133,7 @@ constexpr int kBuckets = 256;
 __global__ __launch_bounds__(1024) void k_bucket(ScoreArgs A, int32_t slot_begin,
                                                  int32_t *__restrict__ pos_out) {
   extern __shared__ __attribute__((aligned(16))) double dyn_lds[];
-  __shared__ int cnt[16 * kBuckets];
+  __shared__ uint32_t cnt[16 * kBuckets / 2];  // (16-bit pairs: stable_bucket_scatter)
   __shared__ double red_lo[16], red_hi[16];
   const int s = blockIdx.z;
   const int slot = row_slot(A, s, slot_begin, A.n_slots - slot_begin, blockIdx.y);
@@ -693,7 +694,8 @@ hipError_t launch_draw(const ScoreArgs &a, bool table, hipStream_t st) {
 hipError_t launch_draw_sorted(const ScoreArgs &a, bool small_table, bool fast, int32_t *pos_out,
                               hipStream_t st) {
   if (a.n_slots <= 0 || a.n_suggest <= 0 || a.n_cand <= 0) return hipSuccess;
-  const unsigned gx = (unsigned)((a.n_cand + kSortedBlock - 1) / kSortedBlock);
+  const int64_t sbk = (int64_t)1 << a.sort_log2;
+  const unsigned gx = (unsigned)((a.n_cand + sbk - 1) / sbk);
   const dim3 g(gx, (unsigned)a.slot_rows, a.n_suggest);
   // fewer blocks than ~2 per CU: 1024-thread blocks (a 256-thread block is 1
   // wave per SIMD; the launch is then bound by one block's latency)
@@ -707,12 +709,12 @@ hipError_t launch_draw_sorted(const ScoreArgs &a, bool small_table, bool fast, i
       else k_draw_sorted_wide<kTabCap><<<g, kWideDrawThreads, 0, st>>>(a, pos_out);
     }
   } else if (fast) {
-    if (small_table) k_draw_sorted_fast<kFuseTab><<<g, kDrawThreads, 0, st>>>(a, pos_out);
-    else k_draw_sorted_fast<kTabCap><<<g, kDrawThreads, 0, st>>>(a, pos_out);
+    if (small_table) k_draw_sorted_fast<kFuseTab><<<g, kSortThreads, 0, st>>>(a, pos_out);
+    else k_draw_sorted_fast<kTabCap><<<g, kSortThreads, 0, st>>>(a, pos_out);
   } else if (small_table) {
-    k_draw_sorted<kFuseTab><<<g, kDrawThreads, 0, st>>>(a, pos_out);
+    k_draw_sorted<kFuseTab><<<g, kSortThreads, 0, st>>>(a, pos_out);
   } else {
-    k_draw_sorted<kTabCap><<<g, kDrawThreads, 0, st>>>(a, pos_out);
+    k_draw_sorted<kTabCap><<<g, kSortThreads, 0, st>>>(a, pos_out);
   }
   return hipGetLastError();
 }
@@ -720,7 +722,8 @@ hipError_t launch_draw_sorted(const ScoreArgs &a, bool small_table, bool fast, i
 hipError_t launch_sort_ext(const ScoreArgs &a, const double *src, int32_t *pos_out,
                            hipStream_t st) {
   if (a.n_slots <= 0 || a.n_suggest != 1 || a.n_cand <= 0) return hipSuccess;
-  const unsigned gx = (unsigned)((a.n_cand + kSortedBlock - 1) / kSortedBlock);
+  const int64_t sbk = (int64_t)1 << a.sort_log2;
+  const unsigned gx = (unsigned)((a.n_cand + sbk - 1) / sbk);
   k_sort_ext<<<dim3(gx, a.n_slots, 1), kDrawThreads, 0, st>>>(a, src, pos_out);
   return hipGetLastError();
 }

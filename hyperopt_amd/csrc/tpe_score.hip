@@ -1768,8 +1768,10 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
   const int wvs = __builtin_amdgcn_readfirstlane(wave);
   int64_t wt0 = (int64_t)tile * tile_cands(KIND) + (WT ? wvs * 64 * KR : 0);
   if constexpr (kind_wave_lse(KIND)) {
-    constexpr int SBB = kSortedBlock / tile_cands(KIND);  // blocks per sort block
-    static_assert(SBB * tile_cands(KIND) == kSortedBlock, "blocks tile the sort block");
+    static_assert((kSortedBlock >> kSortLog2Large) == 1 &&
+                      (1 << kSortLog2Small) % tile_cands(KIND) == 0,
+                  "blocks tile the sort block");
+    const int SBB = (1 << A.sort_log2) / tile_cands(KIND);  // blocks per sort block
     const int sb = tile / SBB, q = tile % SBB;
     const int nbs = min(SBB, ntiles - sb * SBB);
     wt0 = ((int64_t)sb * SBB * kWaves + q + (int64_t)nbs * wvs) * 64 * KR;

@@ -31,9 +31,10 @@ extern "C" {
  * results byte for byte, as long as every part takes the same draw path (the
  * large-draw value-bucketed path runs at >= 2^22 draws per call).  Large
  * draws are value-bucketed in blocks of this many consecutive global
- * candidate indices, and a candidate's pruned log-sum-exp depends on its
- * block.  Unaligned splits still agree under the north-star tie rule. */
-#define TPE_SHARD_ALIGN 4096
+ * candidate indices (of 4096 for suggestions of <= 2^18 candidates, whose
+ * block boundaries are among these), and a candidate's pruned log-sum-exp
+ * depends on its block.  Unaligned splits still agree under the north-star tie rule. */
+#define TPE_SHARD_ALIGN 8192
 
 /* ---- status codes ---------------------------------------------------- */
 #define TPE_OK 0

@@ -451,8 +451,8 @@ def test_config5_bench_shape_multichunk_batch_vs_oracle():
     index (broadcast_best returns samples[best], tpe.py:756-757), its score
     is the oracle's lpdf difference at that value (1e-6), and suggestion s
     equals the single-seed fit_suggest([seed_s], 1e6) (one chunk) byte for
-    byte -- chunk boundaries are multiples of the 4096-candidate sorted-draw
-    block, so no pruned sum depends on the chunking."""
+    byte -- chunk boundaries are multiples of the sorted-draw block
+    (TPE_SHARD_ALIGN), so no pruned sum depends on the chunking."""
     import bench
     dom, losses, vals, act = bench.build_workload('cfg2')
     hps, conds, pprior = dom.space.engine_tables()
@@ -520,7 +520,7 @@ def test_chunk_budget_env_identical_results():
     """TPE_CHUNK_MB (candidate buffer per scoring chunk): a 64 MB budget runs
     a 1e6-candidate config-2 suggest in 3 chunks (accumulated winners), the
     default in one -- byte-identical results (chunk boundaries are multiples
-    of the 4096-candidate sorted-draw block)."""
+    of the sorted-draw block, TPE_SHARD_ALIGN)."""
     code = """
 import sys, numpy as np
 sys.path.insert(0, 'tests')

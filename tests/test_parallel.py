@@ -177,10 +177,10 @@ def _gpu_worker(rank, world, port, outdir, n_cand):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('n_cand', [5000, 24, 4096])
+@pytest.mark.parametrize('n_cand', [10000, 24, 4096])
 def test_sharded_suggest_two_ranks_equals_single_device(n_cand):
     """Two ranks on one GPU equal one device.  24 and 4096 candidates leave
-    rank 1 an empty shard (4096-aligned shards): its records must say
+    rank 1 an empty shard (8192-aligned shards): its records must say
     "nothing here" (NaN, -1, inactive) and not leak a previous suggest's
     winners into the merge (tpe.py:750-759: no samples, no value)."""
     import torch.multiprocessing as mp
