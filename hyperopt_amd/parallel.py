@@ -57,18 +57,20 @@ def suggestion_slice(n_suggest: int, rank: int, world: int):
     return range(b, b + c)
 
 
-def gather_records(local, group=None):
+def gather_records(local, group=None, out=None):
     """All-gather a rank's flat byte tensor of result records.
 
     Returns one contiguous tensor [world * local.numel()] in rank order, the
-    [world][S][P] layout ``tpe_plan_merge`` expects.  Uses the fused
+    [world][S][P] layout ``tpe_plan_merge`` expects (into ``out`` when given:
+    a preallocated buffer of that size on the same device).  Uses the fused
     ``all_gather_into_tensor`` (one RCCL call) where the backend has it and a
     list all-gather otherwise (gloo on CPU)."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
     if local.is_cuda and dist.get_backend(group) == 'nccl':
-        out = torch.empty(world * local.numel(), dtype=local.dtype, device=local.device)
+        if out is None:
+            out = torch.empty(world * local.numel(), dtype=local.dtype, device=local.device)
         dist.all_gather_into_tensor(out, local, group=group)
         return out
     # gloo: stage through host memory (CPU tests; several ranks on one GPU)
@@ -136,7 +138,8 @@ class ShardedSuggest(object):
         # copies and the collective: stream 0 would mean "the engine's own
         # stream" at the C ABI and leave torch unordered with it
         self.stream = torch.cuda.Stream(self.device)
-        self.gather = lambda t: gather_records(t, self.group)
+        self.gather = lambda t, out=None: gather_records(t, self.group, out)
+        self._bufs = {}  # S -> (local records, gathered records): reused per call
 
     def fit(self, **kw):
         """tpe_plan_fit on the sharded stream (ordered before the next
@@ -153,14 +156,24 @@ class ShardedSuggest(object):
         stream = self.stream.cuda_stream
         self.stream.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self.stream):
-            local = torch.empty(S * P * RECORD_BYTES, dtype=torch.uint8, device=self.device)
+            # (the record buffers are allocated once per batch size: the
+            # exchange of a level is then one all-gather and one merge launch,
+            # nothing allocated on the host path between them)
+            bufs = self._bufs.get(S)
+            if bufs is None:
+                nb = S * P * RECORD_BYTES
+                bufs = (torch.empty(nb, dtype=torch.uint8, device=self.device),
+                        torch.empty(self.world * nb, dtype=torch.uint8, device=self.device))
+                self._bufs[S] = bufs
+            local, gbuf = bufs
+            lptr, gptr = local.data_ptr(), gbuf.data_ptr()
             for level in range(self.plan.n_levels):
                 self.plan.suggest(seeds, count, cand_begin=begin, level=level,
-                                  out=local.data_ptr(), stream=stream, n_total=int(n_cand))
-                gathered = self.gather(local)
-                self.plan.merge(gathered.data_ptr(), self.world, level, out=local.data_ptr(),
+                                  out=lptr, stream=stream, n_total=int(n_cand))
+                gathered = self.gather(local, gbuf)
+                self.plan.merge(gathered.data_ptr(), self.world, level, out=lptr,
                                 stream=stream, n_suggest=S)
-            if not fetch:
+            if not fetch:  # (the device records: overwritten by the next suggest of S)
                 torch.cuda.current_stream(self.device).wait_stream(self.stream)
                 return local
             return local.cpu().numpy().view(E.RESULT_DTYPE).reshape(S, P)

@@ -10,7 +10,11 @@ Prints one JSON line:
   single_ms      plan.fit_suggest (one device, no exchange)
   sharded_ms     ShardedSuggest.fit + suggest at world 1 (levels + exchange)
   exchange_us    per suggest: n_levels x (all_gather_into_tensor + merge),
-                 timed alone on the sharded stream with HIP events
+                 timed alone on the sharded stream with HIP events, issued
+                 back to back (bound by the host's issue when that is longer)
+  exchange_device_us  the same on a stream held by a sleep kernel while the
+                 host queues them: the device time of the exchange alone
+  exchange_host_issue_us  the host's issue time per suggest (perf_counter)
   fit_ms         plan.fit alone (every rank repeats it)
 usage: python tools/exchange_time.py --config cfg2|cfg3|cfg4 [--reps N]
 """
@@ -72,28 +76,48 @@ def main():
     # the exchange alone, on the sharded stream, events on that stream
     S, P = 1, plan.n_hp
     local = torch.empty(S * P * parallel.RECORD_BYTES, dtype=torch.uint8, device='cuda')
+    gbuf = torch.empty(sh.world * local.numel(), dtype=torch.uint8, device='cuda')
     sh.suggest([7], n_cand, fetch=False)
     torch.cuda.synchronize()
     nx = 200
+
+    def exchange_loop(n):
+        for _ in range(n):
+            for level in range(plan.n_levels):
+                g = sh.gather(local, gbuf)
+                plan.merge(g.data_ptr(), sh.world, level, out=local.data_ptr(),
+                           stream=sh.stream.cuda_stream, n_suggest=S)
+
     with torch.cuda.stream(sh.stream):
         a = torch.cuda.Event(enable_timing=True)
         b = torch.cuda.Event(enable_timing=True)
-        for warm in (True, False):
-            if not warm:
-                a.record(sh.stream)
-            for _ in range(5 if warm else nx):
-                for level in range(plan.n_levels):
-                    g = sh.gather(local)
-                    plan.merge(g.data_ptr(), sh.world, level, out=local.data_ptr(),
-                               stream=sh.stream.cuda_stream, n_suggest=S)
-            if not warm:
-                b.record(sh.stream)
-    torch.cuda.synchronize()
-    exch_us = 1e3 * a.elapsed_time(b) / nx
+        exchange_loop(5)
+        # (1) back to back as the host issues them (host-issue-bound when
+        # the device work is shorter than the issue)
+        a.record(sh.stream)
+        exchange_loop(nx)
+        b.record(sh.stream)
+        torch.cuda.synchronize()
+        exch_us = 1e3 * a.elapsed_time(b) / nx
+        # (2) device time alone: the stream is held by a sleep kernel while
+        # the host queues the exchanges, so the events see them back to back
+        # on the device (what a level costs when its suggest's kernels keep
+        # the device busy while the host issues the exchange, configs 3-5)
+        torch.cuda._sleep(int(2e8))
+        a.record(sh.stream)
+        import time
+        t0 = time.perf_counter()
+        exchange_loop(nx)
+        host_us = 1e6 * (time.perf_counter() - t0) / nx
+        b.record(sh.stream)
+        torch.cuda.synchronize()
+        dev_us = 1e3 * a.elapsed_time(b) / nx
     print(json.dumps(dict(config=args.config, n_cand=n_cand, n_levels=plan.n_levels, n_hp=P,
                           record_bytes_per_rank=S * P * parallel.RECORD_BYTES,
                           single_ms=single, sharded_ms=sharded_ms, fit_ms=fit_ms,
                           exchange_us_per_suggest=exch_us,
+                          exchange_device_us_per_suggest=dev_us,
+                          exchange_host_issue_us_per_suggest=host_us,
                           note='world 1 over RCCL: the fixed part of the exchange '
                                '(collective launch + kernel, k_merge), no xGMI transfer')))
     dist.destroy_process_group()
