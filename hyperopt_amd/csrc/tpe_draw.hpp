@@ -486,15 +486,18 @@ __device__ __forceinline__ uint64_t lanes_equal8(uint32_t d, bool v) {
   return __ballot(v) & ~(((uint64_t)mhi << 32) | mlo);
 }
 
-template <int NW, typename Dest>
-__device__ __forceinline__ void stable_bucket_scatter(const unsigned char *bk, int n, uint32_t *cnt,
-                                                      Dest dest) {
+// counts, then per (bucket, wave) output bases in cnt (16-bit halves); every
+// thread of the block calls it.  Returns the wave's row range [r0, r1).
+template <int NW>
+__device__ __forceinline__ void bucket_bases(const unsigned char *bk, int n, uint32_t *cnt,
+                                             int &r0, int &r1) {
   // counts and bases per (wave, bucket) are < 2^16 (n <= kSortedBlock): two
   // buckets per 32-bit LDS word, bucket b in half b & 1 of word b >> 1
   static_assert(kSortedBlock < 65536, "16-bit bucket counts");
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int per = ((n + NW * 64 - 1) / (NW * 64)) * 64;
-  const int r0 = w * per, r1 = min(n, r0 + per);
+  r0 = w * per;
+  r1 = min(n, r0 + per);
   uint32_t *mine = cnt + w * (kSortBuckets / 2);
   for (int b = lane; b < kSortBuckets / 2; b += 64) mine[b] = 0u;
   // (a wave's LDS ops complete in order: no barrier between its own rows)
@@ -538,19 +541,81 @@ __device__ __forceinline__ void stable_bucket_scatter(const unsigned char *bk, i
     }
   }
   __syncthreads();
+}
+
+// the destination of element i of the wave's current row (its bucket's base
+// for the wave plus its rank among the row's earlier lanes of that bucket),
+// and the bucket's base moved past the row's members
+__device__ __forceinline__ int bucket_rank(uint32_t *mine, uint32_t d, bool v) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t mt = lanes_equal8(d, v);
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  const int sh = (int)(d & 1) * 16;
+  const int p = (int)((mine[d >> 1] >> sh) & 0xffffu) + __popcll(mt & lt);
+  // (leaders of the two buckets of one word may update it together: atomic)
+  if (v && lane == __ffsll((long long)mt) - 1)
+    __hip_atomic_fetch_add(&mine[d >> 1], (uint32_t)__popcll(mt) << sh, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+  return p;
+}
+
+template <int NW, typename Dest>
+__device__ __forceinline__ void stable_bucket_scatter(const unsigned char *bk, int n, uint32_t *cnt,
+                                                      Dest dest) {
+  int r0, r1;
+  bucket_bases<NW>(bk, n, cnt, r0, r1);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t *mine = cnt + w * (kSortBuckets / 2);
   for (int base = r0; base < r1; base += 64) {
     const int i = base + lane;
     const bool v = i < r1;
     const uint32_t d = v ? bk[i] : 0u;
-    const uint64_t mt = lanes_equal8(d, v);
-    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    const int sh = (int)(d & 1) * 16;
-    if (v) dest(i, (int)((mine[d >> 1] >> sh) & 0xffffu) + __popcll(mt & lt));
-    // (leaders of the two buckets of one word may update it together: atomic)
-    if (v && lane == __ffsll((long long)mt) - 1)
-      __hip_atomic_fetch_add(&mine[d >> 1], (uint32_t)__popcll(mt) << sh, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_WORKGROUP);
+    const int p = bucket_rank(mine, d, v);
+    if (v) dest(i, p);
   }
+}
+
+// The same order, written with coalesced stores: each lane keeps its rows'
+// values and destinations in registers (at most MAXR rows per wave), the
+// values are permuted inside LDS (xs, in place between barriers), written
+// in destination order, and then xs holds the source positions for the
+// position write.  (The scattered stores of stable_bucket_scatter -- 64
+// lines per store instruction -- were a third of k_draw_sorted's time.)
+template <int NW, int MAXR>
+__device__ __forceinline__ void stable_bucket_permute(const unsigned char *bk, int n, uint32_t *cnt,
+                                                      double *xs, double *__restrict__ out,
+                                                      int32_t *__restrict__ po, int64_t base) {
+  int r0, r1;
+  bucket_bases<NW>(bk, n, cnt, r0, r1);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t *mine = cnt + w * (kSortBuckets / 2);
+  double xv[MAXR];
+  int pd[MAXR];
+#pragma unroll
+  for (int j = 0; j < MAXR; ++j) {
+    pd[j] = -1;
+    xv[j] = 0.0;
+    if (r0 + 64 * j < r1) {  // (wave-uniform)
+      const int i = r0 + 64 * j + lane;
+      const bool v = i < r1;
+      const uint32_t d = v ? bk[i] : 0u;
+      const int p = bucket_rank(mine, d, v);
+      if (v) { pd[j] = p; xv[j] = xs[i]; }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < MAXR; ++j)
+    if (pd[j] >= 0) xs[pd[j]] = xv[j];
+  __syncthreads();
+  for (int p = threadIdx.x; p < n; p += NW * 64) out[p] = xs[p];
+  __syncthreads();
+  int32_t *src = reinterpret_cast<int32_t *>(xs);
+#pragma unroll
+  for (int j = 0; j < MAXR; ++j)
+    if (pd[j] >= 0) src[pd[j]] = r0 + 64 * j + lane;
+  __syncthreads();
+  for (int p = threadIdx.x; p < n; p += NW * 64) po[p] = (int32_t)(base + src[p]);
 }
 
 
@@ -669,10 +734,14 @@ __device__ __forceinline__ void sorted_block_body(const ScoreArgs &A, int slot, 
   __syncthreads();
   // scatter into the block's slice, stable
   int32_t *po = pos_out + off;
-  stable_bucket_scatter<NT / 64>(L.bk, n, L.cnt, [&](int i, int p) {
-    out[p] = L.xs[i];
-    po[p] = (int32_t)(base + i);
-  });
+  if constexpr (NT >= 512) {
+    stable_bucket_permute<NT / 64, kSortedBlock / NT>(L.bk, n, L.cnt, L.xs, out, po, base);
+  } else {
+    stable_bucket_scatter<NT / 64>(L.bk, n, L.cnt, [&](int i, int p) {
+      out[p] = L.xs[i];
+      po[p] = (int32_t)(base + i);
+    });
+  }
 }
 
 }  // namespace tpe
