@@ -29,8 +29,8 @@ KIND = {0: 'lse_gmm', 1: 'lse_lgmm', 2: 'erf_gmm', 3: 'erf_lgmm', 4: 'categorica
 
 def short(name):
     if 'k_score' in name:   # k_score<erf, census>: the census variants run in
-        if ', true>' in name or 'k_score_wave<true>' in name:  # the census pass
-            return 'k_score_census'
+        if ', true>' in name or 'k_score_wave<true' in name or 'k_score_wave1<true' in name:
+            return 'k_score_census'  # (the census pass)
         if 'k_score_wave' in name:
             return 'k_score_wave'
         return 'k_score_erf' if 'k_score<true, false>' in name else 'k_score'
