@@ -695,6 +695,14 @@ ScoreArgs base_args(tpe_plan *p, int64_t n_sug) {
 // form covers 72 % of the live chunks at 0.6 VALU per pair, the 8-wide 99 %
 // at ~1.7; at N = 3000, 36 % against 98 %.)  A function of the plan and its
 // history length only, so tpe_plan_fit and fit_suggest write the same table.
+// TPE_MOM16_MIN_K: the 16-wide threshold (A/B; default kMom16MinK)
+static double mom16_min_k() {
+  static const double v = [] {
+    const char *e = std::getenv("TPE_MOM16_MIN_K");
+    return e ? std::atof(e) : (double)kMom16MinK;
+  }();
+  return v;
+}
 int32_t mom_width(const tpe_plan *p) {
   if (!moment_on()) return 0;
   double kmax = 0.0;
@@ -702,7 +710,7 @@ int32_t mom_width(const tpe_plan *p) {
     const int k = score_kind(p->hps[i]);
     if (k == KIND_LSE_G || k == KIND_LSE_L) kmax = std::max(kmax, (double)p->n * p->act_frac[i]);
   }
-  if (kmax >= (double)kMom16MinK) return 16;
+  if (kmax >= mom16_min_k()) return 16;
   if (kmax >= (double)lse_shift_min()) return 8;
   return 0;
 }
