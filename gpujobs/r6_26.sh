@@ -1,0 +1,7 @@
+set -euo pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r6_26; mkdir -p $O
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/exch_trace -o run -- python -u tools/exchange_time.py --config cfg2 > $O/exch.log 2>&1
+python tools/rocpd_stats.py $O/exch_trace > $O/rocpd.log 2>&1
+find $O -name '*.db' -delete
+echo done
