@@ -214,16 +214,21 @@ __device__ __forceinline__ double erfcinv_fast(double y) {
   pc = fmaf(pc, wc, -0.00417768164f);
   pc = fmaf(pc, wc, 0.246640727f);
   pc = fmaf(pc, wc, 1.50140941f);
-  const float wt = __builtin_sqrtf(w) - 3.0f;
-  float pt = -0.000200214257f;
-  pt = fmaf(pt, wt, 0.000100950558f);
-  pt = fmaf(pt, wt, 0.00134934322f);
-  pt = fmaf(pt, wt, -0.00367342844f);
-  pt = fmaf(pt, wt, 0.00573950773f);
-  pt = fmaf(pt, wt, -0.0076224613f);
-  pt = fmaf(pt, wt, 0.00943887047f);
-  pt = fmaf(pt, wt, 1.00167406f);
-  pt = fmaf(pt, wt, 2.83297682f);
+  // (the tail polynomial only when some lane of the wave needs it: w >= 5
+  // means y < ~3.4e-3, so most waves skip it; a select, not a lane branch)
+  float pt = pc;
+  if (__builtin_amdgcn_ballot_w64(!(w < 5.0f))) {
+    const float wt = __builtin_sqrtf(w) - 3.0f;
+    pt = -0.000200214257f;
+    pt = fmaf(pt, wt, 0.000100950558f);
+    pt = fmaf(pt, wt, 0.00134934322f);
+    pt = fmaf(pt, wt, -0.00367342844f);
+    pt = fmaf(pt, wt, 0.00573950773f);
+    pt = fmaf(pt, wt, -0.0076224613f);
+    pt = fmaf(pt, wt, 0.00943887047f);
+    pt = fmaf(pt, wt, 1.00167406f);
+    pt = fmaf(pt, wt, 2.83297682f);
+  }
   const double p = (double)(w < 5.0f ? pc : pt);
   return p * (1.0 - y);
 }
