@@ -83,6 +83,15 @@ static bool publish_fuse_on() {
 // and config 5 543 -> 536 ms per step without it -- the waves' first envelope
 // reads waited on those loads, and the tables are L2-resident after the first
 // blocks anyway
+// TPE_TIGHTEN=0: wave tiles keep lse_window's skip threshold (no tightening
+// from the block of the highest bound) -- A/B
+static bool tighten_on() {
+  static const bool on = [] {
+    const char *e = std::getenv("TPE_TIGHTEN");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
 static bool l2_warm_on() {
   static const bool on = [] {
     const char *e = std::getenv("TPE_L2_WARM");
@@ -684,6 +693,7 @@ ScoreArgs base_args(tpe_plan *p, int64_t n_sug) {
   a.lse_mom = p->mom_w;
   a.lse_momh = p->mom_w == 16 && p->mom_h ? 1 : 0;
   a.l2_warm = l2_warm_on() ? 1 : 0;
+  a.lse_tight = tighten_on() ? 1 : 0;
   return a;
 }
 

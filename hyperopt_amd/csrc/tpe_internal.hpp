@@ -327,6 +327,7 @@ struct ScoreArgs {
                              // for below mixtures of 1 .. kFuseTab components (lookup_inline)
   int64_t lookup_seg;        // candidates per lookup-scan block (set by the lookup launch)
   int32_t l2_warm;           // scoring tiles touch their mixtures' coefficient lines first
+  int32_t lse_tight;         // wave tiles tighten the skip threshold from the top block (default 1)
                              // (one load per 128-B line; TPE_L2_WARM=1, A/B; default off)
   int32_t tile_draw;         // tiny unsorted draws: every tile draws its own candidates
                              // (k_score_tdraw; no k_draw launch, nothing written)

@@ -279,6 +279,7 @@ struct Stage {
   LF4 *env;    // [blocks] envelopes (the Coef w-rows' first 16 B)
   LC32 *c32;   // [blocks] block-local fp32 blocks
   const float4 *genv;  // the slot's compact envelope table (CoefEnv, global; null: w-rows)
+  int tight = 1;       // tighten the threshold from the top block (ScoreArgs::lse_tight)
 };
 constexpr int kStageBlocks = 224;  // blocks of both mixtures a workgroup stages (32 KB)
 struct StageSmem {
@@ -755,7 +756,7 @@ __device__ __forceinline__ bool lse_chunks_shifted(KDbl *__restrict__ cs,
     // lse_window started from; the skip bound then holds as before
     const uint64_t at = __ballot(bmax == wmax && barg >= 0);
     const int kb = __shfl(barg, at ? __builtin_ctzll(at) : 0, 64);
-    if (kb >= 0) {
+    if (kb >= 0 && stg.tight) {
       const int kbu = __builtin_amdgcn_readfirstlane(kb);
       double lo = INFINITY;
       bool done = false;
@@ -1907,6 +1908,10 @@ __device__ __forceinline__ void score_tile(const ScoreArgs &A, SM &sm, int slot,
         bool shifted = false;
         Stage stv{};
         stv.genv = A.coefe ? A.coefe + (mix ? sa : sb) * (A.kcap / kCoefBlock) : nullptr;
+        // (the tightening pays where the pass-2 rounds are many: mixtures of
+        // the range-search size -- config 4 78.7 against 79.5 ms without it;
+        // at K ~ 1e3 it costs more than it prunes, config 5 474.7 vs 471.2)
+        stv.tight = A.lse_tight && K >= kRangeMinK;
         if constexpr (STAGE) {
           stv.env = (LF4 *)(sm.stg.env + (mix ? nbb : 0));
           stv.c32 = (LC32 *)(sm.stg.c32 + (mix ? nbb : 0));
