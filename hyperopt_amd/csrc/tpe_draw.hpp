@@ -633,6 +633,15 @@ __device__ __forceinline__ bool lookup_inline(const ScoreArgs &A, int K) {
   return A.lookup_draw && K >= 1 && K <= kFuseTab;
 }
 
+// The bucketing key of a sorted block: the value, or for log-scale slots
+// its fp32 log2 (v_log_f32 of the value rounded to fp32: buckets only group
+// candidates, so the key needs no more than fp32 and one instruction --
+// round 5's fp64 fast_log cost ~30 VALU, twice per LGMM candidate).  Draws
+// and given candidates (k_sort_ext) bucket through this same function.
+__device__ __forceinline__ double sort_key(double x, bool lg) {
+  return lg ? (double)__builtin_amdgcn_logf((float)x) : x;
+}
+
 template <int CAP, int NT>
 struct SortedDrawLds {
   DrawTableT<CAP> T;
@@ -680,7 +689,7 @@ __device__ __forceinline__ void sorted_block_body(const ScoreArgs &A, int slot, 
       return;
     }
     L.xs[i] = x;
-    const double key = lg ? fast_log(x) : x;
+    const double key = sort_key(x, lg);
     if (fabs(key) < INFINITY) { lo = fmin(lo, key); hi = fmax(hi, key); }
   };
   // bounded continuous slots with a table (config 4 / 5's hps): the table
@@ -731,7 +740,7 @@ __device__ __forceinline__ void sorted_block_body(const ScoreArgs &A, int slot, 
   for (int w = 0; w < NT / 64; ++w) { lo = fmin(lo, L.red[0][w]); hi = fmax(hi, L.red[1][w]); }
   const double scale = hi > lo ? (double)kSortBuckets / (hi - lo) : 0.0;
   for (int i = t; i < n; i += NT) {
-    const double key = lg ? fast_log(L.xs[i]) : L.xs[i];
+    const double key = sort_key(L.xs[i], lg);
     int b = kSortBuckets - 1;
     if (fabs(key) < INFINITY) b = min(kSortBuckets - 1, max(0, (int)((key - lo) * scale)));
     L.bk[i] = (unsigned char)b;
