@@ -1,0 +1,25 @@
+set -euo pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r6_33; mkdir -p $O
+P="--no-cpu-baseline --no-e2e"
+rc=0; timeout -k 10 900 python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu tests/ > $O/tests.log 2>&1 || rc=$?
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.txt 2>&1
+timeout -k 10 600 python -u bench.py > $O/b_default.json 2> $O/b_default.err
+timeout -k 10 300 python -u bench.py --config cfg5 --steps 2 --warmup 1 $P > $O/b_cfg5.json 2> $O/b_cfg5.err
+timeout -k 10 300 python -u bench.py --config cfg3 --steps 50 $P > $O/b_cfg3.json 2> $O/b_cfg3.err
+timeout -k 10 300 python -u bench.py --config cfg2 --steps 100 $P > $O/b_cfg2.json 2> $O/b_cfg2.err
+SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
+for c in cfg4 cfg5 cfg3 cfg2; do
+  S="--steps 1 --warmup 1"; [ $c = cfg3 ] || [ $c = cfg2 ] && S="--steps 20 --warmup 2"
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/${c}_trace -o run -- python -u bench.py --config $c $S $P > $O/${c}_trace.log 2>&1
+  timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $O/${c}_fetch -o run -- python -u bench.py --config $c $S $P > $O/${c}_fetch.log 2>&1
+  timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $O/${c}_write -o run -- python -u bench.py --config $c $S $P > $O/${c}_write.log 2>&1
+  timeout -s KILL 300 rocprofv3 --pmc $SQ -d $O/${c}_sqa -o run -- python -u bench.py --config $c $S $P > $O/${c}_sqa.log 2>&1
+done
+python tools/rocpd_stats.py $O/*_trace $O/*_fetch $O/*_write > $O/rocpd.log 2>&1
+for c in cfg4 cfg5 cfg3 cfg2; do python tools/prof_summary.py --dirs rd6g $c $O/${c}_trace $O/${c}_fetch $O/${c}_write >> $O/summary.log 2>&1; done
+python tools/sq_summary.py profiles/rd6g_sq.json cfg4=$O/cfg4_sqa cfg5=$O/cfg5_sqa cfg3=$O/cfg3_sqa cfg2=$O/cfg2_sqa > $O/sq.log 2>&1
+cp traffic.json profiles/rd6g_*.json profiles/rd6g_*.csv $O/
+find $O -name '*.db' -size +4M -delete
+echo done
