@@ -1,7 +1,7 @@
 """Parity of the production scoring form of large draws (GPU).
 
 At config 4 almost every evaluated (candidate, component) pair runs in the
-large-draw form: candidates value-bucketed in 4096-candidate blocks
+large-draw form: candidates value-bucketed in 8192-candidate blocks
 (k_draw_sorted), log-sum-exp component blocks whose terms are provably below
 2^-(27 + log2 K) of the lane maximum skipped, and one exponent per wave
 (``lse_chunks_shifted``: prune mode 2 with an fp64 quadratic, mode 3 -- the

@@ -101,7 +101,7 @@ def main(cfg, n_cand):
             sel = bend >= 0
             print('block ends (last wave loop): mean %.1f us, max %.1f us (max / mean %.2f)' %
                   (bend[sel].mean(), bend[sel].max(), bend[sel].max() / bend[sel].mean()))
-            # loop time by the wave's place in its 4096-candidate sort block
+            # loop time by the wave's place in its sort block
             # (dense value windows), from the tile mapping of tpe_score.hip
             if (ws[:, :, 2:4] > 0).all(axis=2)[okw].any():
                 ok4 = okw & (ws[:, :, 2] > 0) & (ws[:, :, 3] > 0)
