@@ -495,17 +495,29 @@ class Plan(object):
             e.check(e.lib.tpe_plan_get_results(self.p, res.ctypes.data, 0, None))
         return res
 
+    def get_results(self, out, stream=None):
+        """Copy the last suggest's records to the device pointer ``out``
+        (tpe_plan_get_results, stream-ordered)."""
+        e = self.engine
+        with e.lock:
+            e.check(e.lib.tpe_plan_get_results(self.p, out, 1, stream))
+
     def results_device_ptr(self):
         return self.engine.lib.tpe_plan_results_device(self.p)
 
-    def merge(self, gathered_ptr, world, level, out=None, stream=None, n_suggest=1):
+    def merge(self, gathered_ptr, world, level, out=None, stream=None, n_suggest=1,
+              in_place=False):
+        """tpe_plan_merge; in_place: ``out`` (device) already holds the
+        level's suggest records (suggest(..., out=out)), only the merged
+        slots are stored into it (out_on_device 2, no copy launch)."""
         e = self.engine
         host = out is None
         res = np.empty((n_suggest, self.n_hp), dtype=RESULT_DTYPE) if host else None
         optr = res.ctypes.data if host else out
+        mode = 0 if host else (2 if in_place else 1)
         with e.lock:
             e.check(e.lib.tpe_plan_merge(self.p, gathered_ptr, int(world), int(level), optr,
-                                         0 if host else 1, stream))
+                                         mode, stream))
         return res
 
     def score_candidates(self, hp, x, sorted_mode=None, want_llik=True):

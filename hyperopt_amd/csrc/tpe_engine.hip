@@ -1956,8 +1956,18 @@ int tpe_plan_merge(tpe_plan_t p, const tpe_result *gathered, int32_t world, int3
   CKH(hipSetDevice(h->device));
   hipStream_t st = pick_stream(h, stream);
   const int32_t ns = (int32_t)p->levels[level].size();
+  // out_on_device 2: out already holds this plan's records but for the
+  // level's merged slots (the level's tpe_plan_suggest_shard wrote them
+  // there); k_merge stores those slots into out too, so no copy launch
+  // follows the merge
+  const bool direct = out && out_on_device == 2;
   CKH(launch_merge(p->d_level_hps + p->level_off[level], ns, (int32_t)p->last_nsug, p->P, world,
-                   reinterpret_cast<const Partial *>(gathered), p->d_results, st));
+                   reinterpret_cast<const Partial *>(gathered), p->d_results, st,
+                   direct ? reinterpret_cast<Partial *>(out) : nullptr));
+  if (direct) {
+    p->pub_fired = false;
+    return TPE_OK;
+  }
   return copy_results(h, p, p->last_nsug, out, out_on_device, st);
 }
 

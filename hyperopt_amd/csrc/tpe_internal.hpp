@@ -472,7 +472,7 @@ hipError_t launch_publish(const void *src, void *dst, size_t bytes, uint64_t *fl
 hipError_t launch_merge(const int32_t *level_hps, int32_t n_slots,
                         int32_t n_suggest, int32_t n_hp, int32_t world,
                         const Partial *gathered, Partial *results,
-                        hipStream_t st);
+                        hipStream_t st, Partial *out2 = nullptr);
 hipError_t launch_sample(const tpe_hp *hp_dev, const double *mw,
                          const double *mmu, const double *msig,
                          const MixInfo *info, uint64_t seed, uint64_t stream,

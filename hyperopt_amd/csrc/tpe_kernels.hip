@@ -187,12 +187,14 @@ __global__ __launch_bounds__(1024) void k_bucket(ScoreArgs A, int32_t slot_begin
   });
 }
 
-// cross-device merge of gathered [world][S][P] results
+// cross-device merge of gathered [world][S][P] results; out2 (optional, may
+// alias g): a device copy of the caller's records, the merged slots stored
+// there as well, so the exchange needs no copy launch after the merge
 __global__ __launch_bounds__(64) void k_merge(const int32_t *__restrict__ level_hps,
                                               int32_t n_slots, int32_t n_suggest,
                                               int32_t n_hp, int32_t world,
-                                              const Partial *__restrict__ g,
-                                              Partial *__restrict__ results) {
+                                              const Partial *g,
+                                              Partial *__restrict__ results, Partial *out2) {
   const int slot = blockIdx.x, s = blockIdx.y;
   const int hp = level_hps[slot];
   double bs_ = NAN, bv_ = NAN;
@@ -206,8 +208,11 @@ __global__ __launch_bounds__(64) void k_merge(const int32_t *__restrict__ level_
   wave_best(bs_, bv_, bi_);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) active |= __shfl_xor(active, o, 64);
-  if (threadIdx.x == 0)
-    results[(int64_t)s * n_hp + hp] = Partial{bs_, bv_, active ? bi_ : -1, active, 0};
+  if (threadIdx.x == 0) {
+    const Partial m{bs_, bv_, active ? bi_ : -1, active, 0};
+    results[(int64_t)s * n_hp + hp] = m;
+    if (out2) out2[(int64_t)s * n_hp + hp] = m;
+  }
 }
 
 __global__ __launch_bounds__(256) void k_sample(const tpe_hp *__restrict__ hpd,
@@ -763,10 +768,10 @@ hipError_t launch_publish(const void *src, void *dst, size_t bytes, uint64_t *fl
 
 hipError_t launch_merge(const int32_t *level_hps, int32_t n_slots, int32_t n_suggest,
                         int32_t n_hp, int32_t world, const Partial *gathered,
-                        Partial *results, hipStream_t st) {
+                        Partial *results, hipStream_t st, Partial *out2) {
   if (n_slots <= 0 || n_suggest <= 0) return hipSuccess;
   k_merge<<<dim3(n_slots, n_suggest), 64, 0, st>>>(level_hps, n_slots, n_suggest, n_hp, world,
-                                                   gathered, results);
+                                                   gathered, results, out2);
   return hipGetLastError();
 }
 

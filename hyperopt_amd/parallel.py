@@ -23,6 +23,8 @@ by a deterministic device merge is both exact and, at these sizes
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 
 from . import _engine as E
@@ -140,6 +142,38 @@ class ShardedSuggest(object):
         self.stream = torch.cuda.Stream(self.device)
         self.gather = lambda t, out=None: gather_records(t, self.group, out)
         self._bufs = {}  # S -> (local records, gathered records): reused per call
+        self._views = {}  # (address, bytes) -> tensor over the plan's records
+        # TPE_EXCHANGE_COPY=1 (A/B): the records copied out of the plan before
+        # the all-gather (the round-6 exchange) instead of gathered in place
+        self.copy_exchange = os.environ.get('TPE_EXCHANGE_COPY') == '1'
+
+    def _plan_records(self, nbytes):
+        """A uint8 tensor over the plan's own device records (the first
+        ``nbytes`` of tpe_plan_results_device, through
+        ``__cuda_array_interface__``), cached per (address, size); None where
+        torch cannot wrap a device pointer (gloo on CPU: the caller copies)."""
+        import torch
+        if self.copy_exchange or self.device.type != 'cuda' or not torch.cuda.is_available():
+            return None
+        ptr = self.plan.results_device_ptr()
+        if not ptr:
+            return None
+        key = (ptr, nbytes)
+        view = self._views.get(key)
+        if view is None and key not in self._views:
+            class _Dev(object):
+                pass
+            d = _Dev()
+            d.__cuda_array_interface__ = {'shape': (nbytes,), 'typestr': '|u1',
+                                          'data': (ptr, False), 'version': 2}
+            try:
+                view = torch.as_tensor(d, device=self.device)
+                if view.data_ptr() != ptr:
+                    view = None
+            except (TypeError, RuntimeError, ValueError):
+                view = None
+            self._views[key] = view
+        return view
 
     def fit(self, **kw):
         """tpe_plan_fit on the sharded stream (ordered before the next
@@ -166,13 +200,20 @@ class ShardedSuggest(object):
                         torch.empty(self.world * nb, dtype=torch.uint8, device=self.device))
                 self._bufs[S] = bufs
             local, gbuf = bufs
-            lptr, gptr = local.data_ptr(), gbuf.data_ptr()
+            lptr = local.data_ptr()
             for level in range(self.plan.n_levels):
-                self.plan.suggest(seeds, count, cand_begin=begin, level=level,
-                                  out=lptr, stream=stream, n_total=int(n_cand))
-                gathered = self.gather(local, gbuf)
+                # the level's records stay in the plan (no copy launch); the
+                # all-gather reads them there and the merge stores the merged
+                # slots both into the plan and into `local` (out_on_device 2)
+                self.plan.suggest(seeds, count, cand_begin=begin, level=level, fetch=False,
+                                  stream=stream, n_total=int(n_cand))
+                mine = self._plan_records(S * P * RECORD_BYTES)
+                if mine is None:        # (no device view: the records copied out)
+                    self.plan.get_results(out=lptr, stream=stream)
+                    mine = local
+                gathered = self.gather(mine, gbuf)
                 self.plan.merge(gathered.data_ptr(), self.world, level, out=lptr,
-                                stream=stream, n_suggest=S)
+                                stream=stream, n_suggest=S, in_place=not self.copy_exchange)
             if not fetch:  # (the device records: overwritten by the next suggest of S)
                 torch.cuda.current_stream(self.device).wait_stream(self.stream)
                 return local

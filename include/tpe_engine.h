@@ -241,7 +241,10 @@ const tpe_result *tpe_plan_results_device(tpe_plan_t p);
 
 /* Multi-device: combine world copies of one level's results ([world][S][P],
  * device memory, e.g. an RCCL all-gather) with numpy argmax semantics and
- * make them the plan's state.                                              */
+ * make them the plan's state.  out_on_device 2: `out` is a device buffer
+ * that already holds the records the level's tpe_plan_suggest_shard copied
+ * out (out_on_device 1); only the level's merged slots are stored into it,
+ * by the merge kernel itself (no copy launch after the merge).             */
 int tpe_plan_merge(tpe_plan_t p, const tpe_result *gathered, int32_t world,
                    int32_t level, tpe_result *out, int32_t out_on_device,
                    void *stream);

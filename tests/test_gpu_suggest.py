@@ -239,6 +239,15 @@ def test_candidate_sharding_invariance_and_device_merge():
     torch.cuda.synchronize()
     np.testing.assert_array_equal(merged['index'], full['index'])
     np.testing.assert_array_equal(merged['value'], full['value'])
+    # in place (out_on_device 2): the merge kernel stores the level's slots
+    # into a device buffer that holds the shard's own records -- the same
+    # bytes as the copy-out merge
+    rec = torch.from_numpy(parts[1].view(np.uint8).reshape(-1).copy()).cuda()
+    plan.merge(raw.data_ptr(), world=2, level=0)
+    plan.merge(raw.data_ptr(), world=2, level=0, out=rec.data_ptr(), in_place=True)
+    torch.cuda.synchronize()
+    got = rec.cpu().numpy().view(merged.dtype).reshape(merged.shape)
+    np.testing.assert_array_equal(got.view(np.uint8), merged.view(np.uint8))
 
 
 def test_fit_suggest_graph_replay_matches_eager():

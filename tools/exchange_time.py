@@ -81,12 +81,20 @@ def main():
     torch.cuda.synchronize()
     nx = 200
 
+    # (the product path: the all-gather reads the plan's own records, the
+    # merge stores the merged slots in place -- ShardedSuggest.suggest;
+    # TPE_EXCHANGE_COPY=1: the round-6 path with a copy launch on each side)
+    copy_path = os.environ.get('TPE_EXCHANGE_COPY') == '1'
+    mine = sh._plan_records(S * P * parallel.RECORD_BYTES)
+
     def exchange_loop(n):
         for _ in range(n):
             for level in range(plan.n_levels):
-                g = sh.gather(local, gbuf)
+                if mine is None:
+                    plan.get_results(out=local.data_ptr(), stream=sh.stream.cuda_stream)
+                g = sh.gather(local if mine is None else mine, gbuf)
                 plan.merge(g.data_ptr(), sh.world, level, out=local.data_ptr(),
-                           stream=sh.stream.cuda_stream, n_suggest=S)
+                           stream=sh.stream.cuda_stream, n_suggest=S, in_place=not copy_path)
 
     with torch.cuda.stream(sh.stream):
         a = torch.cuda.Event(enable_timing=True)
@@ -118,6 +126,7 @@ def main():
                           exchange_us_per_suggest=exch_us,
                           exchange_device_us_per_suggest=dev_us,
                           exchange_host_issue_us_per_suggest=host_us,
+                          plan_view=mine is not None, copy_path=copy_path,
                           note='world 1 over RCCL: the fixed part of the exchange '
                                '(collective launch + kernel, k_merge), no xGMI transfer')))
     dist.destroy_process_group()
