@@ -311,7 +311,7 @@ def main():
     ap.add_argument('--steps', type=int, default=5)
     ap.add_argument('--warmup', type=int, default=1)
     ap.add_argument('--config', default='cfg4', choices=sorted(CONFIGS))
-    ap.add_argument('--batch', type=int, default=16,
+    ap.add_argument('--batch', type=int, default=32,
                     help='cfg5: suggestions per engine call')
     ap.add_argument('--n-cand', type=int, default=0,
                     help='override candidates per suggest (secondary measurements only)')

@@ -2176,7 +2176,12 @@ static bool moment_on() {
 static int64_t chunk_budget() {
   static const int64_t v = [] {
     const char *e = std::getenv("TPE_CHUNK_MB");
-    return (e ? std::atoll(e) : 2048) << 17;  // MB -> doubles (2 GB: 1 % faster than 512 MB at config 4, 2 % at config 5)
+    // MB -> doubles.  8 GB (+ 4 GB of positions): config 4's 1e9 candidates
+    // of a level in one draw + one scoring launch, config 5's 32-suggestion
+    // calls in one chunk -- each launch's tail paid once (config 4 79.3 ->
+    // 78.8 ms, config 5 461.3 -> 454.4 ms per step against 2 GB,
+    // profiles/rd6/r6_46; 2 GB had been 1-2 % faster than 512 MB)
+    return (e ? std::atoll(e) : 8192) << 17;
   }();
   return v;
 }

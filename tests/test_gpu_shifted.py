@@ -442,10 +442,12 @@ def test_config3_categorical_posteriors_bit_exact():
 
 def test_config5_bench_shape_multichunk_batch_vs_oracle():
     """Config 5 exactly as ``bench.py --config cfg5`` runs it: config 2's
-    space and history, one fit_suggest of S = 16 suggestions x 1e6
-    candidates.  That exceeds the 2 GB candidate chunk, so the level runs as
-    several chunks whose winners accumulate (ScoreArgs::accumulate), on
-    value-bucketed sorted draws and wave tiles (tpe_engine.hip run_level).
+    space and history, one fit_suggest of S = 32 suggestions x 1e6
+    candidates, on value-bucketed sorted draws and wave tiles (tpe_engine.hip
+    run_level).  Under a 2 GB candidate chunk (TPE_CHUNK_MB=2048, the child
+    run of test_config5_multichunk_env) the level runs as several chunks
+    whose winners accumulate (ScoreArgs::accumulate); the default 8 GB
+    budget runs it in one.
     The reference serves one id per call (tpe.py:812), so parity is per
     suggestion: every winner's value is the draw at its reported global
     index (broadcast_best returns samples[best], tpe.py:756-757), its score
@@ -459,13 +461,14 @@ def test_config5_bench_shape_multichunk_batch_vs_oracle():
     plan = E.Plan(E.default_engine(), hps, conds, pprior, max_trials=losses.size)
     plan.set_history(losses, vals, act)
     obs = _oracle_obs(dom, losses, vals, act)
-    n, S = 1_000_000, 16
+    n, S = 1_000_000, 32
     seeds = [1_000_003 + 7919 * s for s in range(S)]
     plan.profile(64)
     batch = plan.fit_suggest(seeds, n)
     _, launches, _ = plan.profile_read(0)
     plan.profile(0)
-    assert launches >= 2, 'the batch ran in %d chunk(s): not the bench shape' % launches
+    want = 2 if os.environ.get('TPE_CHUNK_MB') == '2048' else 1
+    assert launches >= want, 'the batch ran in %d chunk(s)' % launches
     dev, orc = [], []
     for s, sd in enumerate(seeds):
         assert batch[s]['active'].all()
@@ -493,6 +496,17 @@ def _child(code, env):
                        capture_output=True, text=True, timeout=280)
     assert r.returncode == 0, r.stderr[-3000:]
     return r.stdout
+
+
+def test_config5_multichunk_env():
+    """The config-5 bench-shape test under a 2 GB candidate chunk
+    (TPE_CHUNK_MB=2048): the 32-suggestion level in several chunks whose
+    winners accumulate, every winner against the oracle and the single-seed
+    suggests byte for byte."""
+    out = _child('import sys, pytest; sys.exit(pytest.main(["-q", "-x", "-m", "gpu", '
+                 '"tests/test_gpu_shifted.py::test_config5_bench_shape_multichunk_batch_vs_oracle"]))',
+                 {'TPE_CHUNK_MB': '2048'})
+    assert '1 passed' in out, out[-2000:]
 
 
 def test_shift_min_env_exact_loop():
