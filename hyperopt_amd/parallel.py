@@ -141,6 +141,10 @@ class ShardedSuggest(object):
         # stream" at the C ABI and leave torch unordered with it
         self.stream = torch.cuda.Stream(self.device)
         self.gather = lambda t, out=None: gather_records(t, self.group, out)
+        # (RCCL: the level's all-gather issued directly -- the backend and
+        # world size looked up once here, not per level on the host path)
+        self._rccl = self.device.type == 'cuda' and dist.get_backend(group) == 'nccl'
+        self._all_gather = dist.all_gather_into_tensor
         self._bufs = {}  # S -> (local records, gathered records): reused per call
         self._views = {}  # (address, bytes) -> tensor over the plan's records
         # TPE_EXCHANGE_COPY=1 (A/B): the records copied out of the plan before
@@ -211,7 +215,11 @@ class ShardedSuggest(object):
                 if mine is None:        # (no device view: the records copied out)
                     self.plan.get_results(out=lptr, stream=stream)
                     mine = local
-                gathered = self.gather(mine, gbuf)
+                if self._rccl and mine.is_cuda:
+                    self._all_gather(gbuf, mine, group=self.group)
+                    gathered = gbuf
+                else:
+                    gathered = self.gather(mine, gbuf)
                 self.plan.merge(gathered.data_ptr(), self.world, level, out=lptr,
                                 stream=stream, n_suggest=S, in_place=not self.copy_exchange)
             if not fetch:  # (the device records: overwritten by the next suggest of S)

@@ -92,7 +92,12 @@ def main():
             for level in range(plan.n_levels):
                 if mine is None:
                     plan.get_results(out=local.data_ptr(), stream=sh.stream.cuda_stream)
-                g = sh.gather(local if mine is None else mine, gbuf)
+                src = local if mine is None else mine
+                if sh._rccl and not copy_path:   # (ShardedSuggest.suggest's issue)
+                    sh._all_gather(gbuf, src, group=sh.group)
+                    g = gbuf
+                else:
+                    g = sh.gather(src, gbuf)
                 plan.merge(g.data_ptr(), sh.world, level, out=local.data_ptr(),
                            stream=sh.stream.cuda_stream, n_suggest=S, in_place=not copy_path)
 
